@@ -1,0 +1,152 @@
+/*
+ * sift_hip.h -- C ABI of libsift_hip.so, the MI355X (gfx950) SIFT detect+compute
+ * library.  Plain C types only: no OpenCV, no C++ and no torch types cross
+ * this boundary, so any FFI (ctypes, cgo, JNI, N-API) can bind it.
+ *
+ * Each entry point names the reference interface it replaces
+ * (canhld94/SIFT-GPU include/sift.hpp, src/sift.cpp).  The C++ drop-in that
+ * restores the reference's own signatures on top of this ABI is
+ * include/sift.hpp (implemented in sift-gpu_amd/cpp/sift_shim.cpp).
+ *
+ * Conventions
+ *  - Every function returns SIFT_OK (0) or a negative SIFT_E_* code; the
+ *    message is available from sift_last_error(ctx).  Nothing calls exit().
+ *  - A context owns device workspace sized at creation for images up to
+ *    max_rows x max_cols and batches up to max_batch, plus one HIP stream.
+ *    A context is not thread-safe: use one per host thread.
+ *  - "host" entry points take and return host memory and synchronise; the
+ *    "_device" / "_batch" entry points take device pointers, enqueue on the
+ *    context stream and return immediately (call sift_sync to wait).
+ *  - Results equal the reference CPU path bit for bit in the default (exact)
+ *    mode.  SIFT_FLAG_FAST selects the separable LDS-tiled pyramid, which is
+ *    not bit-exact.
+ */
+#ifndef SIFT_HIP_H_
+#define SIFT_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIFT_OK 0
+#define SIFT_E_INVALID (-1)   /* bad argument */
+#define SIFT_E_HIP (-2)       /* HIP runtime error */
+#define SIFT_E_CAPACITY (-3)  /* output capacity too small; required count reported */
+#define SIFT_E_SIZE (-4)      /* image/batch larger than the context was created for */
+#define SIFT_E_NOMEM (-5)     /* device allocation failed */
+
+#define SIFT_FLAG_FAST 0x1u     /* separable fused pyramid (not bit-exact) */
+#define SIFT_FLAG_PROFILE 0x2u  /* per-stage HIP-event timing, see sift_get_stage_stats */
+#define SIFT_FLAG_VERBOSE 0x4u  /* print the reference's phase timings (src/sift.cpp:70,80,88) */
+
+#define SIFT_DESC_LEN 128
+#define SIFT_N_SCALES 5         /* Gaussian planes per octave */
+#define SIFT_N_DOG 4            /* DoG planes per octave */
+
+/* Layout-identical to cv::KeyPoint {Point2f pt; float size, angle, response;
+ * int octave, class_id;} = 28 bytes.  octave packs o | layer<<8 | xi<<16
+ * exactly as src/sift.cpp:383 does. */
+typedef struct sift_keypoint {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} sift_keypoint;
+
+typedef struct sift_ctx sift_ctx;
+
+typedef struct sift_stage_stat {
+  char name[32];
+  int launches;
+  double ms;     /* summed device time over launches (HIP events) */
+  double flops;  /* algorithmic flops summed over launches */
+  double bytes;  /* algorithmic HBM bytes summed over launches */
+} sift_stage_stat;
+
+/* ---- context ------------------------------------------------------------ */
+int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsigned flags,
+                    sift_ctx** out);
+int sift_ctx_destroy(sift_ctx* ctx);
+const char* sift_last_error(const sift_ctx* ctx);
+/* Use an external HIP stream (hipStream_t) instead of the context's own. */
+int sift_set_stream(sift_ctx* ctx, void* hip_stream);
+void* sift_get_stream(sift_ctx* ctx);
+int sift_set_flags(sift_ctx* ctx, unsigned flags);
+/* Number of octaves (default 5, the literal at src/sift.cpp:67,68,78). */
+int sift_set_octaves(sift_ctx* ctx, int n_octaves);
+int sift_sync(sift_ctx* ctx);
+const char* sift_version(void);
+
+/* ---- layout helpers ----------------------------------------------------- */
+/* Octave shapes: octave o+1 = Size(cols/2, rows/2) of octave o (src/sift.cpp:254). */
+int sift_octave_shapes(int rows, int cols, int n_octaves, int* orows, int* ocols);
+/* Elements of a packed pyramid (planes back to back, no padding): per = 5
+ * (Gaussian, index o*5+s) or 4 (DoG, index o*4+s). */
+size_t sift_packed_size(int rows, int cols, int n_octaves, int per);
+
+/* ---- full detect + compute ---------------------------------------------- */
+/* Replaces SIFT_NCL (include/sift.hpp:41, src/sift.cpp:59-91).
+ * img: host, rows x cols CV_32FC1 values, row_stride_bytes apart.
+ * kpts/desc: host, capacity cap keypoints / cap x 128 floats.  *n_out gets the
+ * keypoint count; if it exceeds cap, nothing is copied and SIFT_E_CAPACITY is
+ * returned (call again with cap >= *n_out). */
+int sift_detect_compute(sift_ctx* ctx, const float* img, int rows, int cols,
+                        size_t row_stride_bytes, sift_keypoint* kpts, float* desc, int cap,
+                        int* n_out);
+
+/* Batch mode on device-resident images.  d_imgs: batch images
+ * of rows x cols, row_stride elements between rows and img_stride elements
+ * between images.  Outputs (device, caller-owned): keypoints of image b occupy
+ * [d_img_offsets[b], d_img_offsets[b+1]) of d_kpts/d_desc (rows of 128).  Only
+ * the first kp_cap keypoints are written; d_img_offsets[batch] holds the true
+ * total, so a caller detects overflow after sift_sync.  Asynchronous. */
+int sift_detect_compute_batch(sift_ctx* ctx, const float* d_imgs, int batch, int rows, int cols,
+                              size_t row_stride, size_t img_stride, sift_keypoint* d_kpts,
+                              float* d_desc, int kp_cap, int* d_img_offsets);
+
+/* Synthetic integer-exact test images, written on device:
+ * image b uses seed 0x5EED0000 + seed_base + b.  Asynchronous. */
+int sift_synth_images(sift_ctx* ctx, float* d_out, int batch, int rows, int cols,
+                      size_t row_stride, size_t img_stride, int seed_base);
+
+/* ---- sub-module entry points (host memory, synchronous) ----------------- */
+/* Gaussian_Blur (include/sift.hpp:47, src/sift.cpp:123-153). */
+int sift_gaussian_blur(sift_ctx* ctx, const float* src, int rows, int cols, double sigma,
+                       float* dst);
+/* Gaussian_Blur_1D (include/sift.hpp:49, src/sift.cpp:170-217). */
+int sift_gaussian_blur_1d(sift_ctx* ctx, const float* src, int rows, int cols, double sigma,
+                          float* dst);
+/* buildGaussianPyramid (include/sift.hpp:51, src/sift.cpp:229-263); gpyr is
+ * packed, sift_packed_size(rows, cols, n_octaves, 5) floats. */
+int sift_build_gaussian_pyramid(sift_ctx* ctx, const float* img, int rows, int cols,
+                                int n_octaves, float* gpyr);
+/* buildDoGPyramid (include/sift.hpp:55, src/sift.cpp:265-283); packed in/out. */
+int sift_build_dog_pyramid(sift_ctx* ctx, const float* gpyr, int rows, int cols, int n_octaves,
+                           float* dog);
+/* findScaleSpaceExtrema (include/sift.hpp:59, src/sift.cpp:547-577); packed
+ * pyramids in; keypoints out with the same count/capacity rule as above. */
+int sift_find_scale_space_extrema(sift_ctx* ctx, const float* gpyr, const float* dog, int rows,
+                                  int cols, int n_octaves, sift_keypoint* kpts, int cap,
+                                  int* n_out);
+/* calDescriptor (include/sift.hpp:64, src/sift.cpp:733-753). */
+int sift_calc_descriptors(sift_ctx* ctx, const float* gpyr, int rows, int cols, int n_octaves,
+                          const sift_keypoint* kpts, int n, float* desc, int first_octave);
+
+/* ---- self-test ------------------------------------------------------------ */
+/* Evaluates one device arithmetic helper element-wise on host arrays (n
+ * values), for bit-exact checks of the GPU math against the CPU oracle:
+ * op 0 exp32f(a), 1 fastAtan2(a, b) (y = a, x = b, degrees), 2 magnitude(a, b),
+ * 3 (float)cos((double)a), 4 (float)sin((double)a), 5 (float)exp2((double)a),
+ * 6 cvRound(a) (as float), 7 cvFloor(a) (as float). */
+int sift_selftest_math(sift_ctx* ctx, int op, const float* a, const float* b, float* out, int n);
+
+/* ---- profiling ------------------------------------------------------------ */
+/* With SIFT_FLAG_PROFILE: per-stage device time accumulated since the last
+ * reset (synchronises).  Writes up to cap entries, *n gets the count. */
+int sift_get_stage_stats(sift_ctx* ctx, sift_stage_stat* out, int cap, int* n, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIFT_HIP_H_ */

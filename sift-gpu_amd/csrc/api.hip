@@ -1,0 +1,782 @@
+// api.hip -- the C ABI (include/sift_hip.h): context, device workspace,
+// pipeline orchestration on one HIP stream, sub-module entry points and
+// per-stage HIP-event profiling.  Host code only; kernels live in blur.hip,
+// detect.hip and descriptor.hip.
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace sift {
+
+Layout make_layout(int rows, int cols, int n_oct) {
+  Layout L;
+  memset(&L, 0, sizeof(L));
+  L.n_oct = n_oct;
+  L.rows = rows;
+  L.cols = cols;
+  long long g = 0, d = 0;
+  int r = rows, c = cols;
+  for (int o = 0; o < n_oct; ++o) {
+    Octave& O = L.oct[o];
+    O.rows = r;
+    O.cols = c;
+    O.pitch = round_up(c > 0 ? c : 1, 16);
+    const long long plane = (long long)O.rows * O.pitch;
+    for (int s = 0; s < kScales; ++s) O.g_off[s] = g + s * plane;
+    for (int s = 0; s < kDogPer; ++s) O.d_off[s] = d + s * plane;
+    g += kScales * plane;
+    d += kDogPer * plane;
+    r /= 2;  // Size(src.cols/2, src.rows/2), src/sift.cpp:254
+    c /= 2;
+  }
+  L.g_img = g;
+  L.d_img = d;
+  return L;
+}
+
+void host_math_consts(MathConsts* mc) {
+  const double A0 = .9670371139572337719125840413672004409288e-2;
+  const double prescale = 1.4426950408889634073599246810019 * 64;
+  const double maxval = 3000. * 64;
+  mc->e.A4 = (float)(1.000000000000002438532970795181890933776 / A0);
+  mc->e.A3 = (float)(.6931471805521448196800669615864773144641 / A0);
+  mc->e.A2 = (float)(.2402265109513301490103372422686535526573 / A0);
+  mc->e.A1 = (float)(.5550339366753125211915322047004666939128e-1 / A0);
+  mc->e.lo = (float)(-maxval / prescale);
+  mc->e.hi = (float)(maxval / prescale);
+  mc->e.post = (float)(1. / 64);
+  mc->e.prescale = (float)prescale;
+  for (int j = 0; j < 64; ++j) mc->exptab[j] = (float)((double)exp2l((long double)j / 64.0L) * A0);
+  const float deg = (float)(180 / kCvPi);
+  mc->t.p1 = 0.9997878412794807f * deg;
+  mc->t.p3 = -0.3258083974640975f * deg;
+  mc->t.p5 = 0.1555786518463281f * deg;
+  mc->t.p7 = -0.04432655554792128f * deg;
+  mc->t.eps = (float)DBL_EPSILON;
+}
+
+}  // namespace sift
+
+using namespace sift;
+
+namespace {
+
+struct StageRec {
+  int stage;
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+
+const char* const kStageNames[] = {"blur_base", "blur_octave", "decimate", "dog", "extrema",
+                                   "refine_orient", "emit", "descriptor", "upload", "download",
+                                   "blur_1d"};
+enum Stage { ST_BLUR_BASE, ST_BLUR_OCT, ST_DECIMATE, ST_DOG, ST_EXTREMA, ST_REFINE, ST_EMIT,
+             ST_DESC, ST_UPLOAD, ST_DOWNLOAD, ST_BLUR1D, ST_N };
+
+template <typename T>
+hipError_t dmalloc(T** p, size_t count) {
+  return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (count ? count : 1));
+}
+
+}  // namespace
+
+struct sift_ctx {
+  int device = 0;
+  unsigned flags = 0;
+  int n_oct = 5;
+  int max_rows = 0, max_cols = 0, max_batch = 0, max_oct = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  // workspace
+  float* d_in = nullptr;
+  long long in_pitch = 0, in_img = 0;
+  float* d_gpyr = nullptr;
+  float* d_dog = nullptr;
+  float* d_tmp = nullptr;
+  long long gpyr_elems = 0, dog_elems = 0;
+  float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
+  float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
+  size_t coef_gen_cap = 0;
+  int wsz[4] = {0, 0, 0, 0};
+  int w_base = 0;
+  size_t coef_base_off = 0, coef_oct_off = 0;
+  MathConsts* d_mc = nullptr;
+  DetectBufs D{};
+  int blk_cap = 0;
+  int* d_img_off = nullptr;       // [max_batch+1] for the host entry points
+  sift_keypoint* d_kpts = nullptr;
+  float* d_desc = nullptr;
+  int kp_cap = 0;
+  int* d_err = nullptr;
+  // profiling
+  std::vector<StageRec> recs;
+  std::vector<hipEvent_t> pool;
+  double acc_ms[ST_N] = {0}, acc_flops[ST_N] = {0}, acc_bytes[ST_N] = {0};
+  int acc_n[ST_N] = {0};
+};
+
+namespace {
+
+int fail(sift_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(sift_ctx* c, hipError_t e, const char* what) {
+  return fail(c, SIFT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(ctx, expr)                                   \
+  do {                                                       \
+    hipError_t e_ = (expr);                                  \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr); \
+  } while (0)
+
+hipEvent_t get_event(sift_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+struct StageScope {
+  sift_ctx* c;
+  int stage;
+  double flops, bytes;
+  hipEvent_t a = nullptr;
+  StageScope(sift_ctx* c_, int st, double f = 0, double b = 0) : c(c_), stage(st), flops(f), bytes(b) {
+    if (c->flags & SIFT_FLAG_PROFILE) {
+      a = get_event(c);
+      (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~StageScope() {
+    if (a) {
+      hipEvent_t b = get_event(c);
+      (void)hipEventRecord(b, c->stream);
+      c->recs.push_back(StageRec{stage, a, b, flops, bytes});
+    }
+  }
+};
+
+void drain_profile(sift_ctx* c) {
+  if (c->recs.empty()) return;
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& r : c->recs) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, r.a, r.b);
+    c->acc_ms[r.stage] += ms;
+    c->acc_flops[r.stage] += r.flops;
+    c->acc_bytes[r.stage] += r.bytes;
+    c->acc_n[r.stage] += 1;
+    c->pool.push_back(r.a);
+    c->pool.push_back(r.b);
+  }
+  c->recs.clear();
+}
+
+int max_octaves_for(int rows, int cols) {
+  int n = 0;
+  while (n < kMaxOctaves && (rows >> n) >= 1 && (cols >> n) >= 1) ++n;
+  return n;
+}
+
+int check_dims(sift_ctx* c, int rows, int cols, int n_oct, int batch) {
+  if (rows <= 0 || cols <= 0) return fail(c, SIFT_E_INVALID, "image dimensions must be positive");
+  if (n_oct < 1 || n_oct > kMaxOctaves) return fail(c, SIFT_E_INVALID, "n_octaves out of range");
+  if ((rows >> (n_oct - 1)) < 1 || (cols >> (n_oct - 1)) < 1)
+    return fail(c, SIFT_E_INVALID,
+                "image too small: every octave must keep at least one row and column "
+                "(the reference's resize to an empty Size throws)");
+  if (rows > c->max_rows || cols > c->max_cols || batch > c->max_batch || n_oct > c->max_oct)
+    return fail(c, SIFT_E_SIZE, "image/batch exceeds the context's creation limits");
+  if (batch < 1) return fail(c, SIFT_E_INVALID, "batch must be >= 1");
+  return SIFT_OK;
+}
+
+// coefficient scratch for arbitrary sigma
+int ensure_coef_gen(sift_ctx* c, size_t n) {
+  if (n <= c->coef_gen_cap) return SIFT_OK;
+  if (c->d_coef_gen) (void)hipFree(c->d_coef_gen);
+  c->d_coef_gen = nullptr;
+  HIP_TRY(c, dmalloc(&c->d_coef_gen, n));
+  c->coef_gen_cap = n;
+  return SIFT_OK;
+}
+
+int ensure_kp(sift_ctx* c, int need) {
+  if (need <= c->kp_cap) return SIFT_OK;
+  if (c->d_kpts) (void)hipFree(c->d_kpts);
+  if (c->d_desc) (void)hipFree(c->d_desc);
+  c->d_kpts = nullptr;
+  c->d_desc = nullptr;
+  c->kp_cap = 0;
+  HIP_TRY(c, dmalloc(&c->d_kpts, (size_t)need));
+  HIP_TRY(c, dmalloc(&c->d_desc, (size_t)need * kDescLen));
+  c->kp_cap = need;
+  return SIFT_OK;
+}
+
+double plane_px(const Layout& L, int o) { return (double)L.oct[o].rows * L.oct[o].cols; }
+
+// Gaussian pyramid (src/sift.cpp:229-263) + DoG (:265-283) for a batch whose
+// input planes are described by src.  Async on c->stream.
+void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool with_dog) {
+  hipStream_t st = c->stream;
+  {
+    const double px = plane_px(L, 0) * batch;
+    const int k = 2 * c->w_base + 1;
+    StageScope s(c, ST_BLUR_BASE, 2.0 * k * k * px, 8.0 * px);
+    launch_blur_plane(st, c->w_base, c->d_coef + c->coef_base_off, src, c->d_gpyr + L.oct[0].g_off[0],
+                      L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
+  }
+  for (int o = 0; o < L.n_oct; ++o) {
+    const double px = plane_px(L, o) * batch;
+    if (o > 0) {
+      StageScope s(c, ST_DECIMATE, 0, 8.0 * px);
+      launch_decimate(st, L, o, c->d_gpyr, batch);
+    }
+    {
+      double taps = 0;
+      for (int q = 0; q < 4; ++q) taps += (double)(2 * c->wsz[q] + 1) * (2 * c->wsz[q] + 1);
+      StageScope s(c, ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
+      launch_blur_octave(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch);
+    }
+    if (with_dog) {
+      StageScope s(c, ST_DOG, 4.0 * px, 36.0 * px);
+      launch_dog(st, L, o, c->d_gpyr, c->d_dog, batch);
+    }
+  }
+}
+
+void enqueue_detect(sift_ctx* c, const Layout& L, int batch, sift_keypoint* kpts, int kp_cap,
+                    int* img_off) {
+  hipStream_t st = c->stream;
+  {
+    StageScope s(c, ST_EXTREMA);
+    launch_extrema(st, L, c->d_dog, batch, c->D);
+  }
+  {
+    StageScope s(c, ST_REFINE);
+    launch_refine_orient(st, L, c->d_gpyr, c->d_dog, c->d_mc, c->D, batch);
+  }
+  {
+    StageScope s(c, ST_EMIT);
+    launch_emit(st, c->D, batch, kpts, kp_cap, img_off);
+  }
+}
+
+void enqueue_desc(sift_ctx* c, const Layout& L, const sift_keypoint* kpts, const int* img_off,
+                  int batch, int kp_cap, float* desc, int first_octave) {
+  StageScope s(c, ST_DESC);
+  launch_descriptors(c->stream, L, c->d_gpyr, c->d_mc, kpts, img_off, batch, kp_cap, desc,
+                     first_octave, c->d_err);
+}
+
+// After a sync: device-side capacity / assertion checks.
+int check_device_status(sift_ctx* c) {
+  int ct = 0, e = 0;
+  HIP_TRY(c, hipMemcpy(&ct, c->D.cand_total, sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (ct > c->D.cand_cap)
+    return fail(c, SIFT_E_CAPACITY,
+                "candidate capacity " + std::to_string(c->D.cand_cap) + " < required " +
+                    std::to_string(ct) + " (create the context with a larger max size)");
+  if (e) {
+    HIP_TRY(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+    return fail(c, SIFT_E_INVALID,
+                "keypoint octave/layer outside the pyramid (CV_Assert at src/sift.cpp:744)");
+  }
+  return SIFT_OK;
+}
+
+int upload_image(sift_ctx* c, const float* img, int rows, int cols, size_t row_stride_bytes) {
+  StageScope s(c, ST_UPLOAD, 0, 4.0 * rows * cols);
+  HIP_TRY(c, hipMemcpy2DAsync(c->d_in, c->in_pitch * sizeof(float), img, row_stride_bytes,
+                              (size_t)cols * sizeof(float), rows, hipMemcpyHostToDevice, c->stream));
+  return SIFT_OK;
+}
+
+// packed host pyramid <-> pitched device pyramid (image 0)
+int copy_pyramid(sift_ctx* c, const Layout& L, float* dev, const float* host_in, float* host_out,
+                 int per) {
+  size_t off = 0;
+  for (int o = 0; o < L.n_oct; ++o) {
+    const Octave& O = L.oct[o];
+    for (int s = 0; s < per; ++s) {
+      float* d = dev + (per == kScales ? O.g_off[s] : O.d_off[s]);
+      const size_t w = (size_t)O.cols * sizeof(float);
+      if (host_in)
+        HIP_TRY(c, hipMemcpy2DAsync(d, O.pitch * sizeof(float), host_in + off, w, w, O.rows,
+                                    hipMemcpyHostToDevice, c->stream));
+      if (host_out)
+        HIP_TRY(c, hipMemcpy2DAsync(host_out + off, w, d, O.pitch * sizeof(float), w, O.rows,
+                                    hipMemcpyDeviceToHost, c->stream));
+      off += (size_t)O.rows * O.cols;
+    }
+  }
+  return SIFT_OK;
+}
+
+void verbose_phase(sift_ctx* c, const char* what, hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  (void)hipEventSynchronize(b);
+  (void)hipEventElapsedTime(&ms, a, b);
+  printf("%s: %g\n", what, (double)ms);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sift_version(void) { return "sift-hip 0.1 (gfx950, exact mode)"; }
+
+int sift_octave_shapes(int rows, int cols, int n_octaves, int* orows, int* ocols) {
+  if (n_octaves < 1 || n_octaves > kMaxOctaves || !orows || !ocols) return SIFT_E_INVALID;
+  int r = rows, c = cols;
+  for (int o = 0; o < n_octaves; ++o) {
+    orows[o] = r;
+    ocols[o] = c;
+    r /= 2;
+    c /= 2;
+  }
+  return SIFT_OK;
+}
+
+size_t sift_packed_size(int rows, int cols, int n_octaves, int per) {
+  size_t t = 0;
+  int r = rows, c = cols;
+  for (int o = 0; o < n_octaves; ++o) {
+    t += (size_t)per * r * c;
+    r /= 2;
+    c /= 2;
+  }
+  return t;
+}
+
+int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsigned flags,
+                    sift_ctx** out) {
+  if (!out || max_rows < 1 || max_cols < 1 || max_batch < 1) return SIFT_E_INVALID;
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return SIFT_E_HIP;
+  sift_ctx* c = new sift_ctx();
+  c->device = device;
+  c->flags = flags;
+  c->max_rows = max_rows;
+  c->max_cols = max_cols;
+  c->max_batch = max_batch;
+  c->max_oct = max_octaves_for(max_rows, max_cols);
+  auto bail = [&](int code) {
+    sift_ctx_destroy(c);
+    return code;
+  };
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(SIFT_E_HIP);
+  c->own_stream = true;
+  const Layout L = make_layout(max_rows, max_cols, c->max_oct);
+  c->in_pitch = round_up(max_cols, 16);
+  c->in_img = c->in_pitch * max_rows;
+  c->gpyr_elems = L.g_img * max_batch;
+  c->dog_elems = L.d_img * max_batch;
+  if (dmalloc(&c->d_in, (size_t)c->in_img * max_batch) != hipSuccess ||
+      dmalloc(&c->d_gpyr, (size_t)c->gpyr_elems) != hipSuccess ||
+      dmalloc(&c->d_dog, (size_t)c->dog_elems) != hipSuccess ||
+      dmalloc(&c->d_tmp, (size_t)c->in_img) != hipSuccess)
+    return bail(SIFT_E_NOMEM);
+  // Gaussian coefficients: base sigma sqrt(1.6^2 + 0.2^2) (src/sift.cpp:237)
+  // and sig[1..4] (src/sift.cpp:240-245), each through getGaussianKernel(float).
+  std::vector<float> coefs;
+  {
+    const float sb = (float)sqrt(kSigma * kSigma + 0.2 * 0.2);
+    const int ks = gaussian_kernel_host(sb, nullptr);
+    c->w_base = ks / 2;
+    c->coef_base_off = 0;
+    coefs.resize(ks * ks);
+    gaussian_kernel_host(sb, coefs.data());
+    c->coef_oct_off = coefs.size();
+    const double k = pow(2.0, 1.0 / kLayers);
+    for (int i = 1; i < kScales; ++i) {
+      const double tot = pow(k * 1.0, (double)i) * kSigma;
+      const float sg = (float)sqrt(tot * tot - kSigma * kSigma);
+      const int kk = gaussian_kernel_host(sg, nullptr);
+      c->wsz[i - 1] = kk / 2;
+      const size_t at = coefs.size();
+      coefs.resize(at + kk * kk);
+      gaussian_kernel_host(sg, coefs.data() + at);
+    }
+  }
+  if (c->w_base != 4 || c->wsz[0] != 4 || c->wsz[1] != 8 || c->wsz[2] != 12 || c->wsz[3] != 18)
+    return bail(SIFT_E_INVALID);  // the octave kernel is unrolled for these widths
+  MathConsts mc;
+  host_math_consts(&mc);
+  if (dmalloc(&c->d_coef, coefs.size()) != hipSuccess || dmalloc(&c->d_mc, 1) != hipSuccess ||
+      dmalloc(&c->d_err, 1) != hipSuccess)
+    return bail(SIFT_E_NOMEM);
+  if (hipMemcpy(c->d_coef, coefs.data(), coefs.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_mc, &mc, sizeof(mc), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess)
+    return bail(SIFT_E_HIP);
+  // detection workspace
+  const long long px = (long long)max_rows * max_cols;
+  const long long per_img = std::max<long long>(16384, px / 32);
+  const long long cap = per_img * max_batch;
+  if (cap > (1ll << 30)) return bail(SIFT_E_NOMEM);
+  c->D.cand_cap = (int)cap;
+  c->blk_cap = extrema_blocks_per_image(L) * max_batch;
+  const size_t scan_n = (size_t)std::max<long long>(c->blk_cap, cap) + 1;
+  if (dmalloc(&c->D.blk_counts, c->blk_cap) != hipSuccess ||
+      dmalloc(&c->D.cand_total, 1) != hipSuccess ||
+      dmalloc(&c->D.img_cand_off, max_batch + 1) != hipSuccess ||
+      dmalloc(&c->D.cands, (size_t)cap) != hipSuccess ||
+      dmalloc(&c->D.couts, (size_t)cap) != hipSuccess ||
+      dmalloc(&c->D.kp_scan, (size_t)cap + 1) != hipSuccess ||
+      dmalloc(&c->D.kp_total, 1) != hipSuccess || dmalloc(&c->D.npeaks, (size_t)cap) != hipSuccess ||
+      dmalloc(&c->D.scan_tmp, scan_n) != hipSuccess ||
+      dmalloc(&c->d_img_off, max_batch + 1) != hipSuccess)
+    return bail(SIFT_E_NOMEM);
+  if (hipMemset(c->D.cand_total, 0, sizeof(int)) != hipSuccess) return bail(SIFT_E_HIP);
+  if (ensure_kp(c, (int)std::min<long long>(cap * 2, 1 << 28)) != SIFT_OK) return bail(SIFT_E_NOMEM);
+  *out = c;
+  return SIFT_OK;
+}
+
+int sift_ctx_destroy(sift_ctx* c) {
+  if (!c) return SIFT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& r : c->recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : c->pool) (void)hipEventDestroy(e);
+  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_coef, c->d_coef_gen, c->d_mc,
+                  c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
+                  c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->d_img_off,
+                  c->d_kpts, c->d_desc, c->d_err};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return SIFT_OK;
+}
+
+const char* sift_last_error(const sift_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int sift_set_stream(sift_ctx* c, void* s) {
+  if (!c) return SIFT_E_INVALID;
+  if (c->own_stream && c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+  }
+  c->stream = (hipStream_t)s;
+  c->own_stream = false;
+  return SIFT_OK;
+}
+
+void* sift_get_stream(sift_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int sift_set_flags(sift_ctx* c, unsigned flags) {
+  if (!c) return SIFT_E_INVALID;
+  c->flags = flags;
+  return SIFT_OK;
+}
+
+int sift_set_octaves(sift_ctx* c, int n) {
+  if (!c) return SIFT_E_INVALID;
+  if (n < 1 || n > c->max_oct) return fail(c, SIFT_E_INVALID, "n_octaves out of range");
+  c->n_oct = n;
+  return SIFT_OK;
+}
+
+int sift_sync(sift_ctx* c) {
+  if (!c) return SIFT_E_INVALID;
+  (void)hipSetDevice(c->device);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return check_device_status(c);
+}
+
+int sift_synth_images(sift_ctx* c, float* d_out, int batch, int rows, int cols, size_t row_stride,
+                      size_t img_stride, int seed_base) {
+  if (!c || !d_out || batch < 1 || rows < 1 || cols < 1 || row_stride < (size_t)cols)
+    return fail(c, SIFT_E_INVALID, "bad synth arguments");
+  (void)hipSetDevice(c->device);
+  launch_synth(c->stream, d_out, batch, rows, cols, (long long)row_stride, (long long)img_stride,
+               seed_base);
+  HIP_TRY(c, hipGetLastError());
+  return SIFT_OK;
+}
+
+int sift_detect_compute_batch(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
+                              size_t row_stride, size_t img_stride, sift_keypoint* d_kpts,
+                              float* d_desc, int kp_cap, int* d_img_offsets) {
+  if (!c) return SIFT_E_INVALID;
+  int rc = check_dims(c, rows, cols, c->n_oct, batch);
+  if (rc) return rc;
+  if (!d_imgs || !d_kpts || !d_desc || !d_img_offsets || kp_cap < 0 || row_stride < (size_t)cols)
+    return fail(c, SIFT_E_INVALID, "null buffer or bad stride");
+  (void)hipSetDevice(c->device);
+  const Layout L = make_layout(rows, cols, c->n_oct);
+  hipEvent_t v0 = nullptr, v1 = nullptr, v2 = nullptr, v3 = nullptr;
+  const bool verbose = c->flags & SIFT_FLAG_VERBOSE;
+  if (verbose) {
+    v0 = get_event(c), v1 = get_event(c), v2 = get_event(c), v3 = get_event(c);
+    (void)hipEventRecord(v0, c->stream);
+  }
+  enqueue_pyramid(c, L, Plane{d_imgs, (long long)row_stride, (long long)img_stride}, batch, true);
+  if (verbose) (void)hipEventRecord(v1, c->stream);
+  enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets);
+  if (verbose) (void)hipEventRecord(v2, c->stream);
+  enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
+  if (verbose) {
+    (void)hipEventRecord(v3, c->stream);
+    verbose_phase(c, "pyramid construction time", v0, v1);
+    verbose_phase(c, "keypoint localization time", v1, v2);
+    verbose_phase(c, "descriptor extraction time", v2, v3);
+    c->pool.insert(c->pool.end(), {v0, v1, v2, v3});
+  }
+  HIP_TRY(c, hipGetLastError());
+  return SIFT_OK;
+}
+
+int sift_detect_compute(sift_ctx* c, const float* img, int rows, int cols, size_t row_stride_bytes,
+                        sift_keypoint* kpts, float* desc, int cap, int* n_out) {
+  if (!c) return SIFT_E_INVALID;
+  if (!img || !n_out) return fail(c, SIFT_E_INVALID, "null image or n_out");
+  if (row_stride_bytes == 0) row_stride_bytes = (size_t)cols * sizeof(float);
+  int rc = check_dims(c, rows, cols, c->n_oct, 1);
+  if (rc) return rc;
+  (void)hipSetDevice(c->device);
+  if ((rc = upload_image(c, img, rows, cols, row_stride_bytes))) return rc;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    rc = sift_detect_compute_batch(c, c->d_in, 1, rows, cols, c->in_pitch, c->in_img, c->d_kpts,
+                                   c->d_desc, c->kp_cap, c->d_img_off);
+    if (rc) return rc;
+    if ((rc = sift_sync(c))) return rc;
+    int n = 0;
+    HIP_TRY(c, hipMemcpy(&n, c->d_img_off + 1, sizeof(int), hipMemcpyDeviceToHost));
+    if (n > c->kp_cap) {  // grow the internal buffer and run again
+      if ((rc = ensure_kp(c, n))) return rc;
+      continue;
+    }
+    *n_out = n;
+    if (n > cap || (n > 0 && (!kpts || !desc)))
+      return fail(c, SIFT_E_CAPACITY, "keypoint capacity " + std::to_string(cap) +
+                                          " < required " + std::to_string(n));
+    if (n > 0) {
+      StageScope s(c, ST_DOWNLOAD, 0, (28.0 + 512.0) * n);
+      HIP_TRY(c, hipMemcpyAsync(kpts, c->d_kpts, sizeof(sift_keypoint) * n, hipMemcpyDeviceToHost,
+                                c->stream));
+      HIP_TRY(c, hipMemcpyAsync(desc, c->d_desc, sizeof(float) * kDescLen * n,
+                                hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return SIFT_OK;
+  }
+  return fail(c, SIFT_E_CAPACITY, "keypoint buffer growth failed");
+}
+
+int sift_gaussian_blur(sift_ctx* c, const float* src, int rows, int cols, double sigma, float* dst) {
+  if (!c) return SIFT_E_INVALID;
+  if (!src || !dst) return fail(c, SIFT_E_INVALID, "null buffer");
+  int rc = check_dims(c, rows, cols, 1, 1);
+  if (rc) return rc;
+  if (!(sigma > 0) || sigma > 100) return fail(c, SIFT_E_INVALID, "sigma out of range");
+  (void)hipSetDevice(c->device);
+  const int ks = gaussian_kernel_host((float)sigma, nullptr);
+  std::vector<float> k((size_t)ks * ks);
+  gaussian_kernel_host((float)sigma, k.data());
+  if ((rc = ensure_coef_gen(c, k.size()))) return rc;
+  HIP_TRY(c, hipMemcpyAsync(c->d_coef_gen, k.data(), k.size() * sizeof(float), hipMemcpyHostToDevice,
+                            c->stream));
+  if ((rc = upload_image(c, src, rows, cols, (size_t)cols * sizeof(float)))) return rc;
+  {
+    StageScope s(c, ST_BLUR_BASE, 2.0 * ks * ks * rows * cols, 8.0 * rows * cols);
+    launch_blur_plane(c->stream, ks / 2, c->d_coef_gen, Plane{c->d_in, c->in_pitch, c->in_img},
+                      c->d_tmp, c->in_pitch, c->in_img, rows, cols, 1);
+  }
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipMemcpy2DAsync(dst, (size_t)cols * sizeof(float), c->d_tmp, c->in_pitch * sizeof(float),
+                              (size_t)cols * sizeof(float), rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SIFT_OK;
+}
+
+int sift_gaussian_blur_1d(sift_ctx* c, const float* src, int rows, int cols, double sigma,
+                          float* dst) {
+  if (!c) return SIFT_E_INVALID;
+  if (!src || !dst) return fail(c, SIFT_E_INVALID, "null buffer");
+  int rc = check_dims(c, rows, cols, 1, 1);
+  if (rc) return rc;
+  if (!(sigma > 0) || sigma > 100) return fail(c, SIFT_E_INVALID, "sigma out of range");
+  (void)hipSetDevice(c->device);
+  // getGaussianKernel1D(double sigma), src/sift.cpp:157-168
+  const int w = (int)floor(3 * sigma);
+  std::vector<float> k(2 * w + 1);
+  for (int i = -w; i <= w; ++i)
+    k[i + w] = (float)(1. / sqrt(2 * kRefPi * sigma * sigma) *
+                       exp(-((double)i * i) * 1. / (2 * sigma * sigma)));
+  if ((rc = ensure_coef_gen(c, k.size()))) return rc;
+  HIP_TRY(c, hipMemcpyAsync(c->d_coef_gen, k.data(), k.size() * sizeof(float), hipMemcpyHostToDevice,
+                            c->stream));
+  if ((rc = upload_image(c, src, rows, cols, (size_t)cols * sizeof(float)))) return rc;
+  float* out = c->d_gpyr;  // scratch (>= one max-size plane)
+  {
+    StageScope s(c, ST_BLUR1D, 4.0 * (2 * w) * rows * cols, 16.0 * rows * cols);
+    launch_blur_1d(c->stream, w, c->d_coef_gen, Plane{c->d_in, c->in_pitch, c->in_img}, c->d_tmp, out,
+                   c->in_pitch, c->in_img, rows, cols, 1);
+  }
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipMemcpy2DAsync(dst, (size_t)cols * sizeof(float), out, c->in_pitch * sizeof(float),
+                              (size_t)cols * sizeof(float), rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SIFT_OK;
+}
+
+int sift_build_gaussian_pyramid(sift_ctx* c, const float* img, int rows, int cols, int n_octaves,
+                                float* gpyr) {
+  if (!c) return SIFT_E_INVALID;
+  if (!img || !gpyr) return fail(c, SIFT_E_INVALID, "null buffer");
+  int rc = check_dims(c, rows, cols, n_octaves, 1);
+  if (rc) return rc;
+  (void)hipSetDevice(c->device);
+  const Layout L = make_layout(rows, cols, n_octaves);
+  if ((rc = upload_image(c, img, rows, cols, (size_t)cols * sizeof(float)))) return rc;
+  enqueue_pyramid(c, L, Plane{c->d_in, c->in_pitch, c->in_img}, 1, false);
+  HIP_TRY(c, hipGetLastError());
+  if ((rc = copy_pyramid(c, L, c->d_gpyr, nullptr, gpyr, kScales))) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SIFT_OK;
+}
+
+int sift_build_dog_pyramid(sift_ctx* c, const float* gpyr, int rows, int cols, int n_octaves,
+                           float* dog) {
+  if (!c) return SIFT_E_INVALID;
+  if (!gpyr || !dog) return fail(c, SIFT_E_INVALID, "null buffer");
+  int rc = check_dims(c, rows, cols, n_octaves, 1);
+  if (rc) return rc;
+  (void)hipSetDevice(c->device);
+  const Layout L = make_layout(rows, cols, n_octaves);
+  if ((rc = copy_pyramid(c, L, c->d_gpyr, gpyr, nullptr, kScales))) return rc;
+  for (int o = 0; o < L.n_oct; ++o) {
+    StageScope s(c, ST_DOG, 4.0 * plane_px(L, o), 36.0 * plane_px(L, o));
+    launch_dog(c->stream, L, o, c->d_gpyr, c->d_dog, 1);
+  }
+  HIP_TRY(c, hipGetLastError());
+  if ((rc = copy_pyramid(c, L, c->d_dog, nullptr, dog, kDogPer))) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SIFT_OK;
+}
+
+int sift_find_scale_space_extrema(sift_ctx* c, const float* gpyr, const float* dog, int rows,
+                                  int cols, int n_octaves, sift_keypoint* kpts, int cap, int* n_out) {
+  if (!c) return SIFT_E_INVALID;
+  if (!gpyr || !dog || !n_out) return fail(c, SIFT_E_INVALID, "null buffer");
+  int rc = check_dims(c, rows, cols, n_octaves, 1);
+  if (rc) return rc;
+  (void)hipSetDevice(c->device);
+  const Layout L = make_layout(rows, cols, n_octaves);
+  if ((rc = copy_pyramid(c, L, c->d_gpyr, gpyr, nullptr, kScales))) return rc;
+  if ((rc = copy_pyramid(c, L, c->d_dog, dog, nullptr, kDogPer))) return rc;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    enqueue_detect(c, L, 1, c->d_kpts, c->kp_cap, c->d_img_off);
+    HIP_TRY(c, hipGetLastError());
+    if ((rc = sift_sync(c))) return rc;
+    int n = 0;
+    HIP_TRY(c, hipMemcpy(&n, c->d_img_off + 1, sizeof(int), hipMemcpyDeviceToHost));
+    if (n > c->kp_cap) {
+      if ((rc = ensure_kp(c, n))) return rc;
+      continue;
+    }
+    *n_out = n;
+    if (n > cap || (n > 0 && !kpts))
+      return fail(c, SIFT_E_CAPACITY, "keypoint capacity " + std::to_string(cap) +
+                                          " < required " + std::to_string(n));
+    if (n > 0)
+      HIP_TRY(c, hipMemcpy(kpts, c->d_kpts, sizeof(sift_keypoint) * n, hipMemcpyDeviceToHost));
+    return SIFT_OK;
+  }
+  return fail(c, SIFT_E_CAPACITY, "keypoint buffer growth failed");
+}
+
+int sift_calc_descriptors(sift_ctx* c, const float* gpyr, int rows, int cols, int n_octaves,
+                          const sift_keypoint* kpts, int n, float* desc, int first_octave) {
+  if (!c) return SIFT_E_INVALID;
+  if (!gpyr || (n > 0 && (!kpts || !desc)) || n < 0) return fail(c, SIFT_E_INVALID, "null buffer");
+  int rc = check_dims(c, rows, cols, n_octaves, 1);
+  if (rc) return rc;
+  if (n == 0) return SIFT_OK;
+  (void)hipSetDevice(c->device);
+  const Layout L = make_layout(rows, cols, n_octaves);
+  if ((rc = ensure_kp(c, n))) return rc;
+  if ((rc = copy_pyramid(c, L, c->d_gpyr, gpyr, nullptr, kScales))) return rc;
+  const int off[2] = {0, n};
+  HIP_TRY(c, hipMemcpyAsync(c->d_img_off, off, sizeof(off), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->d_kpts, kpts, sizeof(sift_keypoint) * n, hipMemcpyHostToDevice,
+                            c->stream));
+  enqueue_desc(c, L, c->d_kpts, c->d_img_off, 1, c->kp_cap, c->d_desc, first_octave);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if ((rc = check_device_status(c))) return rc;
+  HIP_TRY(c, hipMemcpy(desc, c->d_desc, sizeof(float) * kDescLen * n, hipMemcpyDeviceToHost));
+  return SIFT_OK;
+}
+
+int sift_selftest_math(sift_ctx* c, int op, const float* a, const float* b, float* out, int n) {
+  if (!c) return SIFT_E_INVALID;
+  if (!a || !out || n < 0 || op < 0 || op > 7 || ((op == 1 || op == 2) && !b))
+    return fail(c, SIFT_E_INVALID, "bad selftest arguments");
+  if (n == 0) return SIFT_OK;
+  (void)hipSetDevice(c->device);
+  float *da = nullptr, *db = nullptr, *dout = nullptr;
+  HIP_TRY(c, dmalloc(&da, (size_t)n));
+  HIP_TRY(c, dmalloc(&db, (size_t)n));
+  HIP_TRY(c, dmalloc(&dout, (size_t)n));
+  hipError_t e = hipMemcpy(da, a, sizeof(float) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess && b) e = hipMemcpy(db, b, sizeof(float) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    launch_math_selftest(c->stream, op, da, db, dout, n, c->d_mc);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(float) * n, hipMemcpyDeviceToHost);
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dout);
+  if (e != hipSuccess) return hip_fail(c, e, "sift_selftest_math");
+  return SIFT_OK;
+}
+
+int sift_get_stage_stats(sift_ctx* c, sift_stage_stat* out, int cap, int* n, int reset) {
+  if (!c) return SIFT_E_INVALID;
+  drain_profile(c);
+  int k = 0;
+  for (int s = 0; s < ST_N; ++s) {
+    if (!c->acc_n[s]) continue;
+    if (out && k < cap) {
+      memset(&out[k], 0, sizeof(out[k]));
+      strncpy(out[k].name, kStageNames[s], sizeof(out[k].name) - 1);
+      out[k].launches = c->acc_n[s];
+      out[k].ms = c->acc_ms[s];
+      out[k].flops = c->acc_flops[s];
+      out[k].bytes = c->acc_bytes[s];
+    }
+    ++k;
+  }
+  if (n) *n = k;
+  if (reset)
+    for (int s = 0; s < ST_N; ++s) c->acc_ms[s] = c->acc_flops[s] = c->acc_bytes[s] = c->acc_n[s] = 0;
+  return SIFT_OK;
+}
+
+}  // extern "C"

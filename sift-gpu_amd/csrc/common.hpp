@@ -1,0 +1,207 @@
+// common.hpp -- shared host/device definitions for the gfx950 SIFT library.
+//
+// Everything here that computes is an exact restatement of the reference
+// arithmetic (canhld94/SIFT-GPU src/sift.cpp) and of the OpenCV-4.0 helpers it
+// calls, so that device results equal the CPU path bit for bit.  The whole
+// library is compiled with -ffp-contract=off: every a*b+c below is a separate
+// multiply and add, like the reference's x86-64 build (makefile:25, no -march).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/sift_hip.h"
+
+namespace sift {
+
+// ---- tuning constants, src/sift.cpp:4-47 ---------------------------------
+constexpr int kLayers = 2;          // nOctaveLayers
+constexpr int kScales = 5;          // nScales = nOctaveLayers + 3
+constexpr int kDogPer = 4;          // DoG planes per octave
+constexpr int kBorder = 5;          // SIFT_IMG_BORDER
+constexpr int kMaxInterp = 5;       // SIFT_MAX_INTERP_STEPS
+constexpr int kOriBins = 36;        // SIFT_ORI_HIST_BINS
+constexpr int kMaxPeaks = 18;       // strict local maxima of a 36-bin circle
+constexpr int kDescW = 4;           // SIFT_DESCR_WIDTH
+constexpr int kDescBins = 8;        // SIFT_DESCR_HIST_BINS
+constexpr int kDescLen = 128;
+constexpr int kMaxOctaves = 12;
+constexpr float kDogThreshold = 8.f;  // literal at src/sift.cpp:564
+constexpr double kSigma = 1.6;
+constexpr double kRefPi = 3.14159265359;  // src/sift.cpp:7
+constexpr double kCvPi = 3.1415926535897932384626433832795;
+
+// ---- pyramid layout in HBM ------------------------------------------------
+// Per image: octave-major, 5 Gaussian planes then (separately) 4 DoG planes,
+// each plane rows x pitch floats, pitch = cols rounded up to 16 floats (64 B)
+// so every plane row starts 64-B aligned and float4 access is legal.
+struct Octave {
+  int rows, cols, pitch;
+  int pad_;
+  long long g_off[kScales];   // element offset of Gaussian plane s in the image block
+  long long d_off[kDogPer];   // element offset of DoG plane s in the image block
+};
+
+struct Layout {
+  int n_oct;
+  int rows, cols;
+  int pad_;
+  long long g_img;  // elements per image, Gaussian pyramid
+  long long d_img;  // elements per image, DoG pyramid
+  Octave oct[kMaxOctaves];
+};
+
+inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+Layout make_layout(int rows, int cols, int n_oct);
+
+// ---- candidate / keypoint work records -----------------------------------
+struct Cand {            // one 26-neighbour extremum, in reference scan order
+  int b, ol, r, c;       // image, octave | layer<<8, row, col
+};
+
+struct CandOut {         // result of refine + orientation for one candidate
+  float x, y, size, response;
+  int octave, npeaks, img, pad_;
+  float angle[kMaxPeaks];
+  float pad2_[2];
+};
+
+// ---- OpenCV scalar helpers --------------------------
+__device__ __forceinline__ int cv_round(float v) { return __float2int_rn(v); }
+__device__ __forceinline__ int cv_round_d(double v) { return __double2int_rn(v); }
+__device__ __forceinline__ int cv_floor(float v) {
+  int i = (int)v;
+  return i - (i > v);
+}
+__device__ __forceinline__ float sat_u8(float v) {
+  int iv = cv_round(v);
+  return (float)(iv < 0 ? 0 : iv > 255 ? 255 : iv);
+}
+
+// libm calls on the path, evaluated as (float)f((double)x) on CPU and GPU
+// alike (see oracle/sift_oracle.c for the measured glibc deviation).
+__device__ __forceinline__ float pow2f_cr(float y) { return (float)exp2((double)y); }
+__device__ __forceinline__ float cosf_cr(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float sinf_cr(float x) { return (float)sin((double)x); }
+
+// hal::exp32f, scalar form (EXPTAB_SCALE = 6); tab = 64 floats 2^(j/64)*A0.
+struct ExpConsts {
+  float A1, A2, A3, A4, lo, hi, post, prescale;
+};
+
+__device__ __forceinline__ float exp32f(float v, const float* __restrict__ tab,
+                                        const ExpConsts& k) {
+  v = v < k.lo ? k.lo : v;
+  v = k.hi < v ? k.hi : v;
+  v = v * k.prescale;
+  int vi = cv_round(v);
+  v = (v - (float)vi) * k.post;
+  int t = (vi >> 6) + 127;
+  t = !(t & ~255) ? t : t < 0 ? 0 : 255;
+  float sc = __int_as_float(t << 23);
+  float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
+  return sc * tab[vi & 63] * poly;
+}
+
+// hal::fastAtan2 in degrees.
+struct AtanConsts {
+  float p1, p3, p5, p7, eps;
+};
+
+__device__ __forceinline__ float fast_atan2(float y, float x, const AtanConsts& k) {
+  float ax = fabsf(x), ay = fabsf(y);
+  float mn = ax < ay ? ax : ay, mx = ax < ay ? ay : ax;
+  float c = mn / (mx + k.eps);
+  float c2 = c * c;
+  float a = (((k.p7 * c2 + k.p5) * c2 + k.p3) * c2 + k.p1) * c;
+  if (!(ax >= ay)) a = 90.f - a;
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+__device__ __forceinline__ float magnitude(float x, float y) { return sqrtf(x * x + y * y); }
+
+// Matx33f::solve(b, DECOMP_LU): Cramer's rule with float determinant; a
+// singular matrix yields 0 (OpenCV returns Matx::zeros()).
+__device__ __forceinline__ void solve3(const float a[9], const float b[3], float x[3]) {
+#define A_(i, j) a[(i)*3 + (j)]
+  float d = (float)(A_(0, 0) * (A_(1, 1) * A_(2, 2) - A_(2, 1) * A_(1, 2)) -
+                    A_(0, 1) * (A_(1, 0) * A_(2, 2) - A_(2, 0) * A_(1, 2)) +
+                    A_(0, 2) * (A_(1, 0) * A_(2, 1) - A_(2, 0) * A_(1, 1)));
+  if (d == 0) {
+    x[0] = x[1] = x[2] = 0;
+    return;
+  }
+  d = 1 / d;
+  x[0] = d * (b[0] * (A_(1, 1) * A_(2, 2) - A_(1, 2) * A_(2, 1)) -
+              A_(0, 1) * (b[1] * A_(2, 2) - A_(1, 2) * b[2]) +
+              A_(0, 2) * (b[1] * A_(2, 1) - A_(1, 1) * b[2]));
+  x[1] = d * (A_(0, 0) * (b[1] * A_(2, 2) - A_(1, 2) * b[2]) -
+              b[0] * (A_(1, 0) * A_(2, 2) - A_(1, 2) * A_(2, 0)) +
+              A_(0, 2) * (A_(1, 0) * b[2] - b[1] * A_(2, 0)));
+  x[2] = d * (A_(0, 0) * (A_(1, 1) * b[2] - b[1] * A_(2, 1)) -
+              A_(0, 1) * (A_(1, 0) * b[2] - b[1] * A_(2, 0)) +
+              b[0] * (A_(1, 0) * A_(2, 1) - A_(1, 1) * A_(2, 0)));
+#undef A_
+}
+
+// Host-computed constant block shared by every kernel that needs it.
+struct MathConsts {
+  ExpConsts e;
+  AtanConsts t;
+  float exptab[64];
+};
+
+void host_math_consts(MathConsts* mc);
+
+// ---- host launchers (defined in the .hip files) --------------------------
+struct Plane {          // a device plane (or the input image)
+  const float* p;
+  long long pitch;      // elements per row
+  long long img_stride; // elements per image of the batch
+};
+
+// blur.hip
+int gaussian_kernel_host(float sigma, float* coeff);  // src/sift.cpp:95-108
+void launch_blur_plane(hipStream_t st, int w, const float* coef, Plane src, float* dst,
+                       long long dpitch, long long dimg, int rows, int cols, int batch);
+void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
+                        const int* wsz, int batch);
+void launch_decimate(hipStream_t st, const Layout& L, int o, float* gpyr, int batch);
+void launch_dog(hipStream_t st, const Layout& L, int o, const float* gpyr, float* dog, int batch);
+void launch_blur_1d(hipStream_t st, int w, const float* coef1d, Plane src, float* tmp, float* dst,
+                    long long pitch, long long img, int rows, int cols, int batch);
+void launch_synth(hipStream_t st, float* out, int batch, int rows, int cols, long long pitch,
+                  long long img_stride, int seed_base);
+
+// detect.hip
+struct DetectBufs {
+  int* blk_counts;      // per scan block
+  int* cand_total;      // [1]
+  int* img_cand_off;    // [batch+1]
+  Cand* cands;
+  int cand_cap;
+  CandOut* couts;
+  int* kp_scan;         // per candidate exclusive scan of npeaks, [cand_cap+1]
+  int* kp_total;        // [1]
+  int* npeaks;          // orientation peaks per candidate, [cand_cap]
+  int* scan_tmp;        // scratch for the single-block scan
+};
+int extrema_blocks_per_image(const Layout& L);
+void launch_extrema(hipStream_t st, const Layout& L, const float* dog, int batch, DetectBufs& D);
+void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, const float* dog,
+                          const MathConsts* mc, DetectBufs& D, int batch);
+void launch_emit(hipStream_t st, DetectBufs& D, int batch, sift_keypoint* kpts, int kp_cap,
+                 int* img_kp_off);
+
+// descriptor.hip
+void launch_descriptors(hipStream_t st, const Layout& L, const float* gpyr, const MathConsts* mc,
+                        const sift_keypoint* kpts, const int* img_kp_off, int batch,
+                        int kp_cap, float* desc, int first_octave, int* err_flag);
+void launch_math_selftest(hipStream_t st, int op, const float* a, const float* b, float* out, int n,
+                          const MathConsts* mc);
+
+}  // namespace sift

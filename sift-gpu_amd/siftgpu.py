@@ -1,0 +1,335 @@
+"""Python host binding for libsift_hip.so (MI355X SIFT detect + compute).
+
+Mirrors the reference API (canhld94/SIFT-GPU include/sift.hpp:36-67) with the
+same function names and argument meaning, on numpy arrays, by calling the C ABI
+declared in include/sift_hip.h through ctypes.  There is no CPU fallback: if
+the HIP library cannot be loaded or no GPU is present, every call raises.
+
+    kps, desc = SIFT_NCL(img)                     # src/sift.cpp:59-91
+    dst = Gaussian_Blur(src, sigma)               # src/sift.cpp:123-153
+    dst = Gaussian_Blur_1D(src, sigma)            # src/sift.cpp:170-217
+    gpyr = buildGaussianPyramid(img, nOctaves)    # src/sift.cpp:229-263
+    dog = buildDoGPyramid(gpyr, nOctaves)         # src/sift.cpp:265-283
+    kps = findScaleSpaceExtrema(gpyr, dog, nOctaves)        # :547-577
+    desc = calDescriptor(gpyr, kps, firstOctave)             # :733-753
+
+Pyramids are lists of 2-D float32 planes indexed o*5+s (Gaussian) / o*4+s
+(DoG).  Keypoints are numpy structured arrays laid out like cv::KeyPoint.
+
+`Context` exposes the device-resident batch path used by bench.py; buffers are
+torch tensors (PyTorch is used only for device memory and streams).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsift_hip.so")
+
+SIFT_OK, SIFT_E_INVALID, SIFT_E_HIP, SIFT_E_CAPACITY, SIFT_E_SIZE, SIFT_E_NOMEM = 0, -1, -2, -3, -4, -5
+SIFT_FLAG_FAST, SIFT_FLAG_PROFILE, SIFT_FLAG_VERBOSE = 0x1, 0x2, 0x4
+N_SCALES, N_DOG, DESC_LEN = 5, 4, 128
+
+KEYPOINT_DTYPE = np.dtype(
+    [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+
+class SiftError(RuntimeError):
+    def __init__(self, fn, code, msg):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+class StageStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int), ("ms", ctypes.c_double),
+                ("flops", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def build() -> str:
+    """Compile libsift_hip.so (hipcc, gfx950) in-tree."""
+    subprocess.run(["make", "-s", "-C", HERE, "-j8"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built (run make -C {HERE}); no CPU fallback exists")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, ip, fp, sz = ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_size_t
+        pint = ctypes.POINTER(ctypes.c_int)
+        sigs = {
+            "sift_ctx_create": (ip, [ip, ip, ip, ip, ctypes.c_uint, ctypes.POINTER(vp)]),
+            "sift_ctx_destroy": (ip, [vp]),
+            "sift_last_error": (ctypes.c_char_p, [vp]),
+            "sift_set_stream": (ip, [vp, vp]),
+            "sift_get_stream": (vp, [vp]),
+            "sift_set_flags": (ip, [vp, ctypes.c_uint]),
+            "sift_set_octaves": (ip, [vp, ip]),
+            "sift_sync": (ip, [vp]),
+            "sift_version": (ctypes.c_char_p, []),
+            "sift_octave_shapes": (ip, [ip, ip, ip, pint, pint]),
+            "sift_packed_size": (sz, [ip, ip, ip, ip]),
+            "sift_detect_compute": (ip, [vp, fp, ip, ip, sz, vp, fp, ip, pint]),
+            "sift_detect_compute_batch": (ip, [vp, vp, ip, ip, ip, sz, sz, vp, vp, ip, vp]),
+            "sift_synth_images": (ip, [vp, vp, ip, ip, ip, sz, sz, ip]),
+            "sift_gaussian_blur": (ip, [vp, fp, ip, ip, ctypes.c_double, fp]),
+            "sift_gaussian_blur_1d": (ip, [vp, fp, ip, ip, ctypes.c_double, fp]),
+            "sift_build_gaussian_pyramid": (ip, [vp, fp, ip, ip, ip, fp]),
+            "sift_build_dog_pyramid": (ip, [vp, fp, ip, ip, ip, fp]),
+            "sift_find_scale_space_extrema": (ip, [vp, fp, fp, ip, ip, ip, vp, ip, pint]),
+            "sift_calc_descriptors": (ip, [vp, fp, ip, ip, ip, vp, ip, fp, ip]),
+            "sift_get_stage_stats": (ip, [vp, ctypes.POINTER(StageStat), ip, pint, ip]),
+            "sift_selftest_math": (ip, [vp, ip, fp, fp, fp, ip]),
+        }
+        for name, (res, args) in sigs.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+        return L
+
+
+def _fp(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def octave_shapes(rows: int, cols: int, n_octaves: int = 5):
+    out, r, c = [], rows, cols
+    for _ in range(n_octaves):
+        out.append((r, c))
+        r //= 2
+        c //= 2
+    return out
+
+
+def pack_planes(planes, rows, cols, n_octaves, per) -> np.ndarray:
+    shapes = octave_shapes(rows, cols, n_octaves)
+    if len(planes) < n_octaves * per:
+        raise ValueError("too few planes")
+    parts = []
+    for o, (r, c) in enumerate(shapes):
+        for s in range(per):
+            p = np.ascontiguousarray(planes[o * per + s], np.float32)
+            if p.shape != (r, c):
+                raise ValueError(f"plane {o * per + s} has shape {p.shape}, octave shape is {(r, c)}")
+            parts.append(p.reshape(-1))
+    return np.ascontiguousarray(np.concatenate(parts))
+
+
+def split_planes(packed: np.ndarray, rows, cols, n_octaves, per):
+    planes, off = [], 0
+    for (r, c) in octave_shapes(rows, cols, n_octaves):
+        for _ in range(per):
+            planes.append(packed[off:off + r * c].reshape(r, c))
+            off += r * c
+    return planes
+
+
+class Context:
+    """A device context (one HIP stream, workspace for max_rows x max_cols x max_batch)."""
+
+    def __init__(self, max_rows: int, max_cols: int, max_batch: int = 1, device: int = 0,
+                 flags: int = 0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        rc = self._L.sift_ctx_create(device, max_rows, max_cols, max_batch, flags, ctypes.byref(h))
+        if rc != SIFT_OK:
+            raise SiftError("sift_ctx_create", rc, "could not create a device context (no GPU?)")
+        self.h = h
+        self.max_rows, self.max_cols, self.max_batch, self.device = max_rows, max_cols, max_batch, device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.sift_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, fn, rc):
+        if rc != SIFT_OK:
+            raise SiftError(fn, rc, self._L.sift_last_error(self.h).decode())
+
+    # ---- configuration --------------------------------------------------
+    def set_flags(self, flags):
+        self._check("sift_set_flags", self._L.sift_set_flags(self.h, flags))
+
+    def set_octaves(self, n):
+        self._check("sift_set_octaves", self._L.sift_set_octaves(self.h, n))
+
+    def set_stream(self, stream_handle: int):
+        self._check("sift_set_stream", self._L.sift_set_stream(self.h, ctypes.c_void_p(stream_handle)))
+
+    def sync(self):
+        self._check("sift_sync", self._L.sift_sync(self.h))
+
+    # ---- host-memory API (reference names) ------------------------------
+    def SIFT_NCL(self, img: np.ndarray):
+        img = np.ascontiguousarray(img, np.float32)
+        r, c = img.shape
+        n = ctypes.c_int(0)
+        rc = self._L.sift_detect_compute(self.h, _fp(img), r, c, c * 4, None, None, 0, ctypes.byref(n))
+        if rc not in (SIFT_OK, SIFT_E_CAPACITY):
+            self._check("sift_detect_compute", rc)
+        kps = np.zeros(n.value, KEYPOINT_DTYPE)
+        desc = np.zeros((n.value, DESC_LEN), np.float32)
+        if n.value:
+            rc = self._L.sift_detect_compute(self.h, _fp(img), r, c, c * 4, kps.ctypes.data, _fp(desc),
+                                             n.value, ctypes.byref(n))
+            self._check("sift_detect_compute", rc)
+        return kps, desc
+
+    def Gaussian_Blur(self, src: np.ndarray, sigma: float) -> np.ndarray:
+        src = np.ascontiguousarray(src, np.float32)
+        dst = np.empty_like(src)
+        self._check("sift_gaussian_blur",
+                    self._L.sift_gaussian_blur(self.h, _fp(src), src.shape[0], src.shape[1], float(sigma), _fp(dst)))
+        return dst
+
+    def Gaussian_Blur_1D(self, src: np.ndarray, sigma: float) -> np.ndarray:
+        src = np.ascontiguousarray(src, np.float32)
+        dst = np.empty_like(src)
+        self._check("sift_gaussian_blur_1d",
+                    self._L.sift_gaussian_blur_1d(self.h, _fp(src), src.shape[0], src.shape[1], float(sigma), _fp(dst)))
+        return dst
+
+    def buildGaussianPyramid(self, image: np.ndarray, nOctaves: int = 5):
+        image = np.ascontiguousarray(image, np.float32)
+        r, c = image.shape
+        out = np.empty(self._L.sift_packed_size(r, c, nOctaves, N_SCALES), np.float32)
+        self._check("sift_build_gaussian_pyramid",
+                    self._L.sift_build_gaussian_pyramid(self.h, _fp(image), r, c, nOctaves, _fp(out)))
+        return split_planes(out, r, c, nOctaves, N_SCALES)
+
+    def buildDoGPyramid(self, gpyr, nOctaves: int = 5):
+        r, c = gpyr[0].shape
+        g = pack_planes(gpyr, r, c, nOctaves, N_SCALES)
+        out = np.empty(self._L.sift_packed_size(r, c, nOctaves, N_DOG), np.float32)
+        self._check("sift_build_dog_pyramid",
+                    self._L.sift_build_dog_pyramid(self.h, _fp(g), r, c, nOctaves, _fp(out)))
+        return split_planes(out, r, c, nOctaves, N_DOG)
+
+    def findScaleSpaceExtrema(self, gpyr, dogpyr, nOctaves: int = 5) -> np.ndarray:
+        r, c = gpyr[0].shape
+        g = pack_planes(gpyr, r, c, nOctaves, N_SCALES)
+        d = pack_planes(dogpyr, r, c, nOctaves, N_DOG)
+        n = ctypes.c_int(0)
+        rc = self._L.sift_find_scale_space_extrema(self.h, _fp(g), _fp(d), r, c, nOctaves, None, 0, ctypes.byref(n))
+        if rc not in (SIFT_OK, SIFT_E_CAPACITY):
+            self._check("sift_find_scale_space_extrema", rc)
+        kps = np.zeros(n.value, KEYPOINT_DTYPE)
+        if n.value:
+            rc = self._L.sift_find_scale_space_extrema(self.h, _fp(g), _fp(d), r, c, nOctaves,
+                                                       kps.ctypes.data, n.value, ctypes.byref(n))
+            self._check("sift_find_scale_space_extrema", rc)
+        return kps
+
+    def calDescriptor(self, gpyr, keypoints: np.ndarray, firstOctave: int = 0) -> np.ndarray:
+        r, c = gpyr[0].shape
+        n_oct = len(gpyr) // N_SCALES
+        g = pack_planes(gpyr, r, c, n_oct, N_SCALES)
+        kps = np.ascontiguousarray(keypoints, KEYPOINT_DTYPE)
+        desc = np.zeros((len(kps), DESC_LEN), np.float32)
+        self._check("sift_calc_descriptors",
+                    self._L.sift_calc_descriptors(self.h, _fp(g), r, c, n_oct, kps.ctypes.data, len(kps),
+                                                  _fp(desc), firstOctave))
+        return desc
+
+    # ---- device batch API ------------------------------------------------
+    def synth_images(self, out_ptr: int, batch: int, rows: int, cols: int, row_stride: int,
+                     img_stride: int, seed_base: int = 0):
+        self._check("sift_synth_images",
+                    self._L.sift_synth_images(self.h, ctypes.c_void_p(out_ptr), batch, rows, cols,
+                                              row_stride, img_stride, seed_base))
+
+    def detect_compute_batch(self, imgs_ptr: int, batch: int, rows: int, cols: int, row_stride: int,
+                             img_stride: int, kpts_ptr: int, desc_ptr: int, kp_cap: int, offs_ptr: int):
+        self._check("sift_detect_compute_batch",
+                    self._L.sift_detect_compute_batch(self.h, ctypes.c_void_p(imgs_ptr), batch, rows, cols,
+                                                      row_stride, img_stride, ctypes.c_void_p(kpts_ptr),
+                                                      ctypes.c_void_p(desc_ptr), kp_cap,
+                                                      ctypes.c_void_p(offs_ptr)))
+
+    def selftest_math(self, op: int, a: np.ndarray, b: np.ndarray | None = None) -> np.ndarray:
+        a = np.ascontiguousarray(a, np.float32)
+        bb = np.ascontiguousarray(b if b is not None else a, np.float32)
+        out = np.empty_like(a)
+        self._check("sift_selftest_math",
+                    self._L.sift_selftest_math(self.h, op, _fp(a), _fp(bb), _fp(out), a.size))
+        return out
+
+    def stage_stats(self, reset: bool = True):
+        buf = (StageStat * 32)()
+        n = ctypes.c_int(0)
+        self._check("sift_get_stage_stats",
+                    self._L.sift_get_stage_stats(self.h, buf, 32, ctypes.byref(n), int(reset)))
+        return {buf[i].name.decode(): dict(launches=buf[i].launches, ms=buf[i].ms, flops=buf[i].flops,
+                                           bytes=buf[i].bytes) for i in range(n.value)}
+
+
+# ---- module-level API with the reference's names (one shared context) -------
+_default = None
+
+
+def _ctx(rows, cols):
+    global _default
+    if _default is None or rows > _default.max_rows or cols > _default.max_cols:
+        mr = max(rows, _default.max_rows if _default else 0)
+        mc = max(cols, _default.max_cols if _default else 0)
+        if _default is not None:
+            _default.close()
+        _default = Context(mr, mc, 1, int(os.environ.get("SIFT_HIP_DEVICE", "0")))
+    return _default
+
+
+def SIFT_NCL(image):
+    return _ctx(*image.shape).SIFT_NCL(image)
+
+
+def Gaussian_Blur(src, sigma):
+    return _ctx(*src.shape).Gaussian_Blur(src, sigma)
+
+
+def Gaussian_Blur_1D(src, sigma):
+    return _ctx(*src.shape).Gaussian_Blur_1D(src, sigma)
+
+
+def buildGaussianPyramid(image, nOctaves=5):
+    return _ctx(*image.shape).buildGaussianPyramid(image, nOctaves)
+
+
+def buildDoGPyramid(gpyr, nOctaves=5):
+    return _ctx(*gpyr[0].shape).buildDoGPyramid(gpyr, nOctaves)
+
+
+def findScaleSpaceExtrema(gpyr, dogpyr, nOctaves=5):
+    return _ctx(*gpyr[0].shape).findScaleSpaceExtrema(gpyr, dogpyr, nOctaves)
+
+
+def calDescriptor(gpyr, keypoints, firstOctave=0):
+    return _ctx(*gpyr[0].shape).calDescriptor(gpyr, keypoints, firstOctave)
