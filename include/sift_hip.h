@@ -95,6 +95,12 @@ int sift_detect_compute(sift_ctx* ctx, const float* img, int rows, int cols,
                         size_t row_stride_bytes, sift_keypoint* kpts, float* desc, int cap,
                         int* n_out);
 
+/* Copies the keypoints/descriptors of the last host-API call that produced
+ * them (sift_detect_compute or sift_find_scale_space_extrema) without
+ * recomputing: the second half of the two-call sizing pattern.  desc may be
+ * NULL (extrema only).  SIFT_E_CAPACITY if cap < count (*n_out = count). */
+int sift_copy_results(sift_ctx* ctx, sift_keypoint* kpts, float* desc, int cap, int* n_out);
+
 /* Batch mode on device-resident images.  d_imgs: batch images
  * of rows x cols, row_stride elements between rows and img_stride elements
  * between images.  Outputs (device, caller-owned): keypoints of image b occupy

@@ -117,9 +117,7 @@ void SIFT_NCL(InputArray image, std::vector<KeyPoint>& keypoints, OutputArray de
   descriptors.create(n, SIFT_DESC_LEN, CV_32F);
   Mat d = descriptors.getMat();
   if (n > 0) {
-    rc = sift_detect_compute(c, img.ptr<float>(0), img.rows, img.cols, sizeof(float) * img.cols,
-                             reinterpret_cast<sift_keypoint*>(keypoints.data()), d.ptr<float>(0), n,
-                             &n);
+    rc = sift_copy_results(c, reinterpret_cast<sift_keypoint*>(keypoints.data()), d.ptr<float>(0), n, &n);
     if (rc) raise("SIFT_NCL", rc, c);
   }
 }
@@ -181,8 +179,7 @@ void findScaleSpaceExtrema(std::vector<Mat>& gpyr, std::vector<Mat>& dogpyr,
   keypoints.clear();
   keypoints.resize(n);
   if (n > 0) {
-    rc = sift_find_scale_space_extrema(c, g.data(), d.data(), rows, cols, nOctaves,
-                                       reinterpret_cast<sift_keypoint*>(keypoints.data()), n, &n);
+    rc = sift_copy_results(c, reinterpret_cast<sift_keypoint*>(keypoints.data()), nullptr, n, &n);
     if (rc) raise("findScaleSpaceExtrema", rc, c);
   }
 }

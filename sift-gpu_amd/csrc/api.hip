@@ -115,6 +115,8 @@ struct sift_ctx {
   sift_keypoint* d_kpts = nullptr;
   float* d_desc = nullptr;
   int kp_cap = 0;
+  int last_n = -1;                // keypoints held from the last host call
+  bool last_has_desc = false;
   int* d_err = nullptr;
   // profiling
   std::vector<StageRec> recs;
@@ -517,6 +519,25 @@ int sift_synth_images(sift_ctx* c, float* d_out, int batch, int rows, int cols, 
   return SIFT_OK;
 }
 
+int sift_copy_results(sift_ctx* c, sift_keypoint* kpts, float* desc, int cap, int* n_out) {
+  if (!c) return SIFT_E_INVALID;
+  if (!n_out) return fail(c, SIFT_E_INVALID, "null n_out");
+  if (c->last_n < 0) return fail(c, SIFT_E_INVALID, "no results held: run a host detect call first");
+  const int n = c->last_n;
+  *n_out = n;
+  if (n > cap) return fail(c, SIFT_E_CAPACITY, "keypoint capacity " + std::to_string(cap) +
+                                                   " < required " + std::to_string(n));
+  if (n == 0) return SIFT_OK;
+  if (!kpts || (desc && !c->last_has_desc)) return fail(c, SIFT_E_INVALID, "nothing to copy into");
+  (void)hipSetDevice(c->device);
+  HIP_TRY(c, hipMemcpyAsync(kpts, c->d_kpts, sizeof(sift_keypoint) * n, hipMemcpyDeviceToHost, c->stream));
+  if (desc)
+    HIP_TRY(c, hipMemcpyAsync(desc, c->d_desc, sizeof(float) * kDescLen * n, hipMemcpyDeviceToHost,
+                              c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SIFT_OK;
+}
+
 int sift_detect_compute_batch(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
                               size_t row_stride, size_t img_stride, sift_keypoint* d_kpts,
                               float* d_desc, int kp_cap, int* d_img_offsets) {
@@ -526,6 +547,11 @@ int sift_detect_compute_batch(sift_ctx* c, const float* d_imgs, int batch, int r
   if (!d_imgs || !d_kpts || !d_desc || !d_img_offsets || kp_cap < 0 || row_stride < (size_t)cols)
     return fail(c, SIFT_E_INVALID, "null buffer or bad stride");
   (void)hipSetDevice(c->device);
+  if (d_kpts == c->d_kpts) {
+    // internal buffers (host entry point): results are re-cached by the caller
+  } else {
+    c->last_n = -1;
+  }
   const Layout L = make_layout(rows, cols, c->n_oct);
   hipEvent_t v0 = nullptr, v1 = nullptr, v2 = nullptr, v3 = nullptr;
   const bool verbose = c->flags & SIFT_FLAG_VERBOSE;
@@ -570,6 +596,8 @@ int sift_detect_compute(sift_ctx* c, const float* img, int rows, int cols, size_
       continue;
     }
     *n_out = n;
+    c->last_n = n;
+    c->last_has_desc = true;
     if (n > cap || (n > 0 && (!kpts || !desc)))
       return fail(c, SIFT_E_CAPACITY, "keypoint capacity " + std::to_string(cap) +
                                           " < required " + std::to_string(n));
@@ -699,6 +727,8 @@ int sift_find_scale_space_extrema(sift_ctx* c, const float* gpyr, const float* d
       continue;
     }
     *n_out = n;
+    c->last_n = n;
+    c->last_has_desc = false;
     if (n > cap || (n > 0 && !kpts))
       return fail(c, SIFT_E_CAPACITY, "keypoint capacity " + std::to_string(cap) +
                                           " < required " + std::to_string(n));
@@ -719,6 +749,7 @@ int sift_calc_descriptors(sift_ctx* c, const float* gpyr, int rows, int cols, in
   (void)hipSetDevice(c->device);
   const Layout L = make_layout(rows, cols, n_octaves);
   if ((rc = ensure_kp(c, n))) return rc;
+  c->last_n = -1;  // the internal keypoint buffer is reused below
   if ((rc = copy_pyramid(c, L, c->d_gpyr, gpyr, nullptr, kScales))) return rc;
   const int off[2] = {0, n};
   HIP_TRY(c, hipMemcpyAsync(c->d_img_off, off, sizeof(off), hipMemcpyHostToDevice, c->stream));

@@ -86,6 +86,7 @@ def lib():
             "sift_packed_size": (sz, [ip, ip, ip, ip]),
             "sift_detect_compute": (ip, [vp, fp, ip, ip, sz, vp, fp, ip, pint]),
             "sift_detect_compute_batch": (ip, [vp, vp, ip, ip, ip, sz, sz, vp, vp, ip, vp]),
+            "sift_copy_results": (ip, [vp, vp, fp, ip, pint]),
             "sift_synth_images": (ip, [vp, vp, ip, ip, ip, sz, sz, ip]),
             "sift_gaussian_blur": (ip, [vp, fp, ip, ip, ctypes.c_double, fp]),
             "sift_gaussian_blur_1d": (ip, [vp, fp, ip, ip, ctypes.c_double, fp]),
@@ -199,9 +200,8 @@ class Context:
         kps = np.zeros(n.value, KEYPOINT_DTYPE)
         desc = np.zeros((n.value, DESC_LEN), np.float32)
         if n.value:
-            rc = self._L.sift_detect_compute(self.h, _fp(img), r, c, c * 4, kps.ctypes.data, _fp(desc),
-                                             n.value, ctypes.byref(n))
-            self._check("sift_detect_compute", rc)
+            rc = self._L.sift_copy_results(self.h, kps.ctypes.data, _fp(desc), n.value, ctypes.byref(n))
+            self._check("sift_copy_results", rc)
         return kps, desc
 
     def Gaussian_Blur(self, src: np.ndarray, sigma: float) -> np.ndarray:
@@ -244,9 +244,8 @@ class Context:
             self._check("sift_find_scale_space_extrema", rc)
         kps = np.zeros(n.value, KEYPOINT_DTYPE)
         if n.value:
-            rc = self._L.sift_find_scale_space_extrema(self.h, _fp(g), _fp(d), r, c, nOctaves,
-                                                       kps.ctypes.data, n.value, ctypes.byref(n))
-            self._check("sift_find_scale_space_extrema", rc)
+            rc = self._L.sift_copy_results(self.h, kps.ctypes.data, None, n.value, ctypes.byref(n))
+            self._check("sift_copy_results", rc)
         return kps
 
     def calDescriptor(self, gpyr, keypoints: np.ndarray, firstOctave: int = 0) -> np.ndarray:
