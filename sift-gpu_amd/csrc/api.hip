@@ -101,6 +101,7 @@ struct sift_ctx {
   float* d_gpyr = nullptr;
   float* d_dog = nullptr;
   float* d_tmp = nullptr;
+  float2* d_grad = nullptr;       // per-pixel (magnitude, orientation), gpyr layout
   long long gpyr_elems = 0, dog_elems = 0;
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
@@ -263,16 +264,19 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
   }
 }
 
+// dog_from_gpyr: the fused extrema pass also forms (and writes) the DoG planes
+// from the Gaussian pyramid; otherwise the DoG planes are already resident
+// (sift_find_scale_space_extrema uploads both pyramids).
 void enqueue_detect(sift_ctx* c, const Layout& L, int batch, sift_keypoint* kpts, int kp_cap,
-                    int* img_off) {
+                    int* img_off, bool dog_from_gpyr) {
   hipStream_t st = c->stream;
   {
     StageScope s(c, ST_EXTREMA);
-    launch_extrema(st, L, c->d_dog, batch, c->D);
+    launch_extrema(st, L, c->d_gpyr, c->d_dog, dog_from_gpyr, c->d_grad, c->d_mc, batch, c->D);
   }
   {
     StageScope s(c, ST_REFINE);
-    launch_refine_orient(st, L, c->d_gpyr, c->d_dog, c->d_mc, c->D, batch);
+    launch_refine_orient(st, L, c->d_gpyr, c->d_grad, c->d_dog, c->d_mc, c->D, batch);
   }
   {
     StageScope s(c, ST_EMIT);
@@ -283,7 +287,7 @@ void enqueue_detect(sift_ctx* c, const Layout& L, int batch, sift_keypoint* kpts
 void enqueue_desc(sift_ctx* c, const Layout& L, const sift_keypoint* kpts, const int* img_off,
                   int batch, int kp_cap, float* desc, int first_octave) {
   StageScope s(c, ST_DESC);
-  launch_descriptors(c->stream, L, c->d_gpyr, c->d_mc, kpts, img_off, batch, kp_cap, desc,
+  launch_descriptors(c->stream, L, c->d_grad, c->d_mc, kpts, img_off, batch, kp_cap, desc,
                      first_octave, c->d_err);
 }
 
@@ -394,7 +398,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   if (dmalloc(&c->d_in, (size_t)c->in_img * max_batch) != hipSuccess ||
       dmalloc(&c->d_gpyr, (size_t)c->gpyr_elems) != hipSuccess ||
       dmalloc(&c->d_dog, (size_t)c->dog_elems) != hipSuccess ||
-      dmalloc(&c->d_tmp, (size_t)c->in_img) != hipSuccess)
+      dmalloc(&c->d_tmp, (size_t)c->in_img) != hipSuccess ||
+      dmalloc(&c->d_grad, (size_t)c->gpyr_elems) != hipSuccess)
     return bail(SIFT_E_NOMEM);
   // Gaussian coefficients: base sigma sqrt(1.6^2 + 0.2^2) (src/sift.cpp:237)
   // and sig[1..4] (src/sift.cpp:240-245), each through getGaussianKernel(float).
@@ -435,9 +440,10 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   const long long cap = per_img * max_batch;
   if (cap > (1ll << 30)) return bail(SIFT_E_NOMEM);
   c->D.cand_cap = (int)cap;
-  c->blk_cap = extrema_blocks_per_image(L) * max_batch;
+  c->blk_cap = mask_blocks_per_image(L) * max_batch;
   const size_t scan_n = (size_t)std::max<long long>(c->blk_cap, cap) + 1;
-  if (dmalloc(&c->D.blk_counts, c->blk_cap) != hipSuccess ||
+  if (dmalloc(&c->D.mask, (size_t)mask_words_per_image(L) * max_batch) != hipSuccess ||
+      dmalloc(&c->D.blk_counts, c->blk_cap) != hipSuccess ||
       dmalloc(&c->D.cand_total, 1) != hipSuccess ||
       dmalloc(&c->D.img_cand_off, max_batch + 1) != hipSuccess ||
       dmalloc(&c->D.cands, (size_t)cap) != hipSuccess ||
@@ -462,8 +468,8 @@ int sift_ctx_destroy(sift_ctx* c) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : c->pool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_coef, c->d_coef_gen, c->d_mc,
-                  c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
+  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
+                  c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
                   c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->d_img_off,
                   c->d_kpts, c->d_desc, c->d_err};
   for (void* p : bufs)
@@ -559,9 +565,9 @@ int sift_detect_compute_batch(sift_ctx* c, const float* d_imgs, int batch, int r
     v0 = get_event(c), v1 = get_event(c), v2 = get_event(c), v3 = get_event(c);
     (void)hipEventRecord(v0, c->stream);
   }
-  enqueue_pyramid(c, L, Plane{d_imgs, (long long)row_stride, (long long)img_stride}, batch, true);
+  enqueue_pyramid(c, L, Plane{d_imgs, (long long)row_stride, (long long)img_stride}, batch, false);
   if (verbose) (void)hipEventRecord(v1, c->stream);
-  enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets);
+  enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
   if (verbose) (void)hipEventRecord(v2, c->stream);
   enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
   if (verbose) {
@@ -717,7 +723,7 @@ int sift_find_scale_space_extrema(sift_ctx* c, const float* gpyr, const float* d
   if ((rc = copy_pyramid(c, L, c->d_gpyr, gpyr, nullptr, kScales))) return rc;
   if ((rc = copy_pyramid(c, L, c->d_dog, dog, nullptr, kDogPer))) return rc;
   for (int attempt = 0; attempt < 2; ++attempt) {
-    enqueue_detect(c, L, 1, c->d_kpts, c->kp_cap, c->d_img_off);
+    enqueue_detect(c, L, 1, c->d_kpts, c->kp_cap, c->d_img_off, false);
     HIP_TRY(c, hipGetLastError());
     if ((rc = sift_sync(c))) return rc;
     int n = 0;
@@ -755,6 +761,8 @@ int sift_calc_descriptors(sift_ctx* c, const float* gpyr, int rows, int cols, in
   HIP_TRY(c, hipMemcpyAsync(c->d_img_off, off, sizeof(off), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->d_kpts, kpts, sizeof(sift_keypoint) * n, hipMemcpyHostToDevice,
                             c->stream));
+  // keypoints may name any scale 0..4 (CV_Assert at src/sift.cpp:744): gradients of all five
+  launch_grad(c->stream, L, c->d_gpyr, c->d_grad, 1, 0, kScales - 1, c->d_mc);
   enqueue_desc(c, L, c->d_kpts, c->d_img_off, 1, c->kp_cap, c->d_desc, first_octave);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -179,6 +179,7 @@ void launch_synth(hipStream_t st, float* out, int batch, int rows, int cols, lon
 
 // detect.hip
 struct DetectBufs {
+  unsigned* mask;       // candidate bitmask, mask_words_per_image * batch
   int* blk_counts;      // per scan block
   int* cand_total;      // [1]
   int* img_cand_off;    // [batch+1]
@@ -190,15 +191,19 @@ struct DetectBufs {
   int* npeaks;          // orientation peaks per candidate, [cand_cap]
   int* scan_tmp;        // scratch for the single-block scan
 };
-int extrema_blocks_per_image(const Layout& L);
-void launch_extrema(hipStream_t st, const Layout& L, const float* dog, int batch, DetectBufs& D);
-void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, const float* dog,
-                          const MathConsts* mc, DetectBufs& D, int batch);
+long long mask_words_per_image(const Layout& L);
+int mask_blocks_per_image(const Layout& L);
+void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* dog, bool write_dog,
+                    float2* grad, const MathConsts* mc, int batch, DetectBufs& D);
+void launch_grad(hipStream_t st, const Layout& L, const float* gpyr, float2* grad, int batch, int s_lo,
+                 int s_hi, const MathConsts* mc);
+void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, const float2* grad,
+                          const float* dog, const MathConsts* mc, DetectBufs& D, int batch);
 void launch_emit(hipStream_t st, DetectBufs& D, int batch, sift_keypoint* kpts, int kp_cap,
                  int* img_kp_off);
 
 // descriptor.hip
-void launch_descriptors(hipStream_t st, const Layout& L, const float* gpyr, const MathConsts* mc,
+void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, const MathConsts* mc,
                         const sift_keypoint* kpts, const int* img_kp_off, int batch,
                         int kp_cap, float* desc, int first_octave, int* err_flag);
 void launch_math_selftest(hipStream_t st, int op, const float* a, const float* b, float* out, int n,

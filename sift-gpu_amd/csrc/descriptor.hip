@@ -1,18 +1,25 @@
 // descriptor.hip -- 128-D descriptor (reference src/sift.cpp:579-753) for gfx950.
 //
-// One wave per keypoint.  The reference builds the 6x6x10 trilinear
-// histogram by adding samples in window raster order, so each bin's float
-// sum has a fixed order.  The wave keeps that order:
-//   * the (2r+1)^2 window (r <= 40, so <= 6561 samples) is walked in chunks of
-//     64 raster-consecutive samples, one per lane: rotation, bounds, gradient
-//     (4 neighbour loads), exp32f / fastAtan2 / magnitude and the 8 trilinear
-//     weights are computed in parallel and parked in LDS;
-//   * the chunk's valid samples (a wave-uniform ballot mask) are then added in
-//     lane order; the 8 corners of one sample hit 8 distinct bins, so lanes
-//     0-7 add one corner each -- one LDS read-modify-write per sample;
-//   * fold, 0.2 clamp, uchar quantisation and the RootSIFT-style
-//     normalisation (src/sift.cpp:676-721) keep the reference's sequential
-//     sums (one lane) and run the element-wise parts across the wave.
+// The reference builds a 6x6x10 trilinear histogram by adding window samples
+// in raster order; every bin's float sum must keep that order to be
+// bit-exact.  Design (one wave = 8 keypoints, lanes 8g..8g+7 own keypoint g):
+//
+//  * Samples: only the (i, j) that can pass the rotated-square test
+//    rbin, cbin in (-1, d) are enumerated -- per window row the candidate
+//    j-range is derived from the two slabs |r_rot|, |c_rot| < 2.5 (plus a
+//    margin), so about half of the (2r+1)^2 window is skipped; the exact float
+//    predicate of src/sift.cpp:620-621 still decides each sample.  Gradient
+//    magnitude / orientation per pixel come precomputed (detect.hip), so a
+//    sample is one 8-byte gather + exp32f + the trilinear weights.
+//  * Accumulation by bin ownership: a sample's 8 corners (r0+dr, c0+dc, o0+do)
+//    always have 8 distinct parities (R&1, C&1, O&1).  Lane q of a group owns
+//    every bin of parity q, so each sample hands exactly one corner to each
+//    lane and every bin is updated by one lane only, in sample order -- plain
+//    per-lane LDS read-modify-writes, no atomics, no cross-lane hazards.  The
+//    histogram lives at [qidx][lane] (qidx = (R>>1)*15 + (C>>1)*5 + (O>>1)),
+//    so all 64 lanes of an update hit distinct banks.
+//  * Fold, 0.2 clamp, uchar quantisation, RootSIFT (src/sift.cpp:676-721)
+//    keep the reference's sequential sums (lane 0 of the group).
 #include "common.hpp"
 
 #include <float.h>
@@ -25,11 +32,14 @@ __device__ __forceinline__ void wave_sync_d() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr int kHistLen = (kDescW + 2) * (kDescW + 2) * (kDescBins + 2);  // 360
+constexpr int kGrp = 8;            // keypoints per wave
+constexpr int kQBins = 45;         // bins per parity class: 3 x 3 x 5
+constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
+constexpr int kRecStride = 68;     // LDS row stride of the per-sample corner records
 
 struct DescArgs {
   Layout L;
-  const float* gpyr;
+  const float2* grad;     // per-pixel (magnitude, orientation) planes, gpyr layout
   const MathConsts* mc;
   const sift_keypoint* kpts;
   const int* img_kp_off;  // [batch+1]
@@ -40,50 +50,75 @@ struct DescArgs {
   int* err_flag;
 };
 
-__global__ __launch_bounds__(256) void descriptor_kernel(DescArgs A) {
-  __shared__ float hist[4][kHistLen + 8];
-  __shared__ int ridx[4][64];
-  __shared__ float rval[4][8][64];
-  __shared__ float vec[4][kDescLen];
-  __shared__ float bc[4][4];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+// Narrow [lo, hi] to the j with |j*a + b| < 2.5 (+ margin).
+__device__ __forceinline__ void slab(float a, float b, int& lo, int& hi) {
+  const float lim = 2.5f + 1e-2f;  // margin >> float rounding of r_rot / c_rot
+  if (fabsf(a) < 1e-12f) {
+    if (!(fabsf(b) < lim)) hi = lo - 1;
+    return;
+  }
+  float x0 = (-lim - b) / a, x1 = (lim - b) / a;
+  if (x0 > x1) {
+    const float t = x0;
+    x0 = x1;
+    x1 = t;
+  }
+  lo = max(lo, (int)fmaxf(ceilf(x0), -1e6f));
+  hi = min(hi, (int)fminf(floorf(x1), 1e6f));
+}
+
+__global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
+  __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
+  __shared__ int rbase[kGrp * 8];                   // [group][sample]: r0+1 | (c0+1)<<4 | o0<<8
+  __shared__ __attribute__((aligned(16))) float rval[8 * kRecStride];  // [sample][group][corner]
+  __shared__ int rows_tab[kGrp][kMaxWinRows];       // per row: (jlo + 64) | len << 16
+  __shared__ float bc[kGrp][4];
+  __shared__ float etab[64];
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 3, q = lane & 7;
   const int d = kDescW, nb = kDescBins;
   int n = A.img_kp_off[A.batch];
   if (n > A.kp_cap) n = A.kp_cap;
   const ExpConsts ek = A.mc->e;
-  const AtanConsts ak = A.mc->t;
-  const float* etab = A.mc->exptab;
-  // corner offsets of hist[idx] += v_rco000 ... v_rco111 (src/sift.cpp:665-672)
-  const int coff[8] = {0, 1, nb + 2, nb + 3, (d + 2) * (nb + 2), (d + 2) * (nb + 2) + 1,
-                       (d + 3) * (nb + 2), (d + 3) * (nb + 2) + 1};
-  const int my_off = coff[lane & 7];
+  etab[lane] = A.mc->exptab[lane];
 
-  for (int k = blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
-    // image of keypoint k: offsets are ascending, batch is small
-    int b = 0;
-    while (b + 1 < A.batch && A.img_kp_off[b + 1] <= k) ++b;
-    const sift_keypoint kp = A.kpts[k];
-    // ---- unpackOctave + calDescriptor body, src/sift.cpp:724-751 ----
+  // XCD-aware split (speed only): blocks b and b+8 share an XCD, so XCD x takes
+  // one contiguous eighth of the raster-ordered keypoints and its L2 sees the
+  // overlapping windows of neighbouring keypoints.
+  const int xcd = blockIdx.x & 7, nslot = gridDim.x >> 3, slot = blockIdx.x >> 3;
+  const int per = ((n + 7) / 8 + kGrp - 1) / kGrp * kGrp;
+  const int kend = min(n, (xcd + 1) * per);
+  for (int kb = xcd * per + slot * kGrp; kb < kend; kb += nslot * kGrp) {
+    const int k = kb + g;
+    bool active = k < kend;
+    int b = 0, oi = 0, layer = 0;
+    sift_keypoint kp{};
+    if (active) {
+      while (b + 1 < A.batch && A.img_kp_off[b + 1] <= k) ++b;
+      kp = A.kpts[k];
+      int octave = kp.octave & 255;
+      layer = (kp.octave >> 8) & 255;
+      octave = octave < 128 ? octave : (-128 | octave);
+      oi = octave - A.first_octave;
+      if (oi < 0 || oi >= A.L.n_oct || layer > kLayers + 2) {  // CV_Assert, src/sift.cpp:744
+        if (q == 0) atomicOr(A.err_flag, 1);
+        for (int t = q; t < kDescLen; t += 8) A.desc[(long long)k * kDescLen + t] = 0.f;
+        active = false;
+      }
+    }
+    // ---- unpackOctave + calcSIFTDescriptor setup (src/sift.cpp:724-751, 582-592) ----
     int octave = kp.octave & 255;
-    const int layer = (kp.octave >> 8) & 255;
     octave = octave < 128 ? octave : (-128 | octave);
     const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
-    const int oi = octave - A.first_octave;
-    if (oi < 0 || oi >= A.L.n_oct || layer > kLayers + 2) {  // CV_Assert at :744
-      if (lane == 0) atomicOr(A.err_flag, 1);
-      for (int q = lane; q < kDescLen; q += 64) A.desc[(long long)k * kDescLen + q] = 0.f;
-      continue;
-    }
     const float size = kp.size * scale;
     const float ptx = kp.x * scale, pty = kp.y * scale;
     float ori = 360.f - kp.angle;
     if (fabsf(ori - 360.f) < FLT_EPSILON) ori = 0.f;
     const float scl = size * 0.5f;
-    const Octave& O = A.L.oct[oi];
+    const Octave& O = A.L.oct[active ? oi : 0];
     const long long pitch = O.pitch;
-    const float* img = A.gpyr + b * A.L.g_img + O.g_off[layer];
+    const float2* gimg = A.grad + b * A.L.g_img + O.g_off[active ? layer : 0];
     const int rows = O.rows, cols = O.cols;
-    // ---- calcSIFTDescriptor, src/sift.cpp:579-722 ----
     const int px = cv_round(ptx), py = cv_round(pty);
     float cos_t = cosf_cr(ori * (float)(kCvPi / 180));
     float sin_t = sinf_cr(ori * (float)(kCvPi / 180));
@@ -95,17 +130,53 @@ __global__ __launch_bounds__(256) void descriptor_kernel(DescArgs A) {
     radius = radius < diag ? radius : diag;
     cos_t /= hist_width;
     sin_t /= hist_width;
-    for (int q = lane; q < kHistLen; q += 64) hist[wv][q] = 0.f;
+    const int D = active ? 2 * radius + 1 : 0;
+    const bool table = D <= kMaxWinRows;
+    // ---- per-row candidate j-ranges and the sample count ----
+    int nsamp = 0;
+    if (table) {
+      for (int ri = q; ri < D; ri += 8) {
+        const int i = ri - radius;
+        int lo = max(-radius, 1 - px), hi = min(radius, cols - 2 - px);  // 0 < px + j < cols-1
+        if (!(py + i > 0 && py + i < rows - 1)) hi = lo - 1;
+        slab(sin_t, i * cos_t, lo, hi);     // r_rot = j*sin_t + i*cos_t
+        slab(cos_t, -(i * sin_t), lo, hi);  // c_rot = j*cos_t - i*sin_t
+        const int len = hi >= lo ? hi - lo + 1 : 0;
+        rows_tab[g][ri] = len ? (lo + 64) | (len << 16) : 0;  // lo in [-40, 40] when len > 0
+        nsamp += len;
+      }
+      nsamp += __shfl_xor(nsamp, 1);
+      nsamp += __shfl_xor(nsamp, 2);
+      nsamp += __shfl_xor(nsamp, 4);
+    } else {
+      nsamp = D * D;  // radius > 40 (caller-supplied keypoints): the whole window
+    }
+    for (int t = 0; t < kQBins; ++t) hist[t * 64 + lane] = 0.f;
+    int nmax = nsamp;
+    nmax = max(nmax, __shfl_xor(nmax, 8));
+    nmax = max(nmax, __shfl_xor(nmax, 16));
+    nmax = max(nmax, __shfl_xor(nmax, 32));
     wave_sync_d();
-    const int D = 2 * radius + 1;
-    const int ns = D * D;
-    for (int base = 0; base < ns; base += 64) {
-      const int s = base + lane;
-      bool valid = false;
-      int idx = 0;
+    // lane q walks candidate samples t = q, q+8, ... in raster order (row ri, offset u)
+    int ri = 0, u = q, rlo = -radius, rlen = D;
+    if (table && D > 0) {
+      const int e = rows_tab[g][0];
+      rlo = (e & 0xffff) - 64;
+      rlen = e >> 16;
+    }
+    while (ri < D && u >= rlen) {
+      u -= rlen;
+      if (++ri < D && table) {
+        const int e = rows_tab[g][ri];
+        rlo = (e & 0xffff) - 64;
+        rlen = e >> 16;
+      }
+    }
+    for (int base = 0; base < nmax; base += 8) {
+      int pk = -1;
       float v[8];
-      if (s < ns) {
-        const int i = s / D - radius, j = s % D - radius;
+      if (base + q < nsamp) {
+        const int i = ri - radius, j = rlo + u;
         const float c_rot = j * cos_t - i * sin_t;
         const float r_rot = j * sin_t + i * cos_t;
         float rbin = r_rot + d / 2 - 0.5f;
@@ -113,15 +184,10 @@ __global__ __launch_bounds__(256) void descriptor_kernel(DescArgs A) {
         const int r = py + i, c = px + j;
         if (rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 &&
             c < cols - 1) {
-          valid = true;
-          const float* row = img + (long long)r * pitch;
-          const float dx = (float)(row[c + 1] - row[c - 1]);
-          const float dy = (float)(row[c - pitch] - row[c + pitch]);
+          const float2 mo = gimg[(long long)r * pitch + c];  // (Mag, Ori) of the pixel
           const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab, ek);
-          const float o_deg = fast_atan2(dy, dx, ak);
-          const float mag0 = magnitude(dx, dy);
-          float obin = (o_deg - ori) * bins_per_rad;
-          const float mag = mag0 * w;
+          float obin = (mo.y - ori) * bins_per_rad;
+          const float mag = mo.x * w;
           const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
           int o0 = cv_floor(obin);
           rbin -= r0;
@@ -132,7 +198,7 @@ __global__ __launch_bounds__(256) void descriptor_kernel(DescArgs A) {
           const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
           const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
           const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-          v[7] = v_rc11 * obin;
+          v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
           v[6] = v_rc11 - v[7];
           v[5] = v_rc10 * obin;
           v[4] = v_rc10 - v[5];
@@ -140,67 +206,98 @@ __global__ __launch_bounds__(256) void descriptor_kernel(DescArgs A) {
           v[2] = v_rc01 - v[3];
           v[1] = v_rc00 * obin;
           v[0] = v_rc00 - v[1];
-          idx = ((r0 + 1) * (d + 2) + c0 + 1) * (nb + 2) + o0;
+          pk = (r0 + 1) | ((c0 + 1) << 4) | (o0 << 8);
         }
       }
-      unsigned long long m = __ballot(valid);
-      if (valid) {
-        ridx[wv][lane] = idx;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) rval[wv][q][lane] = v[q];
+      u += 8;  // advance to candidate sample t + 8
+      while (ri < D && u >= rlen) {
+        u -= rlen;
+        if (++ri < D && table) {
+          const int e = rows_tab[g][ri];
+          rlo = (e & 0xffff) - 64;
+          rlen = e >> 16;
+        }
+      }
+      rbase[lane] = pk;
+      if (pk >= 0) {
+        float4* rv = reinterpret_cast<float4*>(rval + q * kRecStride + g * 8);
+        rv[0] = make_float4(v[0], v[1], v[2], v[3]);
+        rv[1] = make_float4(v[4], v[5], v[6], v[7]);
       }
       wave_sync_d();
-      while (m) {  // wave-uniform loop over the chunk's valid samples, in order
-        const int sl = __builtin_ctzll(m);
-        m &= m - 1;
-        if (lane < 8) {
-          const int h = ridx[wv][sl] + my_off;
-          hist[wv][h] = hist[wv][h] + rval[wv][lane][sl];
+      // ordered accumulation: lane q adds the corner of parity q of each sample
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int p = rbase[g * 8 + jj];
+        if (p >= 0) {
+          const int R0 = p & 15, C0 = (p >> 4) & 15, O0 = p >> 8;
+          const int dr = ((q >> 2) ^ R0) & 1, dc = ((q >> 1) ^ C0) & 1, dO = (q ^ O0) & 1;
+          const float val = rval[jj * kRecStride + g * 8 + (dr * 4 + dc * 2 + dO)];
+          const int qi = ((R0 + dr) >> 1) * 15 + ((C0 + dc) >> 1) * 5 + ((O0 + dO) >> 1);
+          hist[qi * 64 + lane] = hist[qi * 64 + lane] + val;
         }
       }
       wave_sync_d();
     }
-    // ---- circular fold + copy (src/sift.cpp:676-684) ----
-    if (lane < d * d) {
-      const int i = lane / d, j = lane % d;
-      const int idx = ((i + 1) * (d + 2) + (j + 1)) * (nb + 2);
-      float* h = hist[wv] + idx;
-      h[0] = h[0] + h[nb];
-      h[1] = h[1] + h[nb + 1];
+    // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
+    float cell[2][8];
 #pragma unroll
-      for (int q = 0; q < nb; ++q) vec[wv][(i * d + j) * nb + q] = h[q];
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int cidx = q + 8 * h2;
+      const int R = cidx / d + 1, C = cidx % d + 1;
+#pragma unroll
+      for (int o = 0; o < nb + 2; ++o) {
+        const int par = ((R & 1) << 2) | ((C & 1) << 1) | (o & 1);
+        const float hv = hist[((R >> 1) * 15 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
+        if (o < nb)
+          cell[h2][o] = hv;
+        else
+          cell[h2][o - nb] = cell[h2][o - nb] + hv;
+      }
     }
+    wave_sync_d();
+    float* dv = hist + g * (kDescLen + 4);  // the 128-vector reuses histogram storage
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int t = 0; t < nb; ++t) dv[(q + 8 * h2) * nb + t] = cell[h2][t];
     wave_sync_d();
     // ---- hysteresis + quantisation + RootSIFT (src/sift.cpp:689-721) ----
-    float* dv = vec[wv];
-    if (lane == 0) {
+    if (q == 0) {
       float nrm2 = 0;
-      for (int q = 0; q < kDescLen; ++q) nrm2 = nrm2 + dv[q] * dv[q];
-      bc[wv][0] = sqrtf(nrm2) * 0.2f;
+      for (int t = 0; t < kDescLen; ++t) nrm2 = nrm2 + dv[t] * dv[t];
+      bc[g][0] = sqrtf(nrm2) * 0.2f;
     }
     wave_sync_d();
-    const float thr = bc[wv][0];
-    for (int q = lane; q < kDescLen; q += 64) dv[q] = dv[q] < thr ? dv[q] : thr;
+    const float thr = bc[g][0];
+    for (int t = q; t < kDescLen; t += 8) dv[t] = dv[t] < thr ? dv[t] : thr;
     wave_sync_d();
-    if (lane == 0) {
+    if (q == 0) {
       float nrm2 = 0;
-      for (int q = 0; q < kDescLen; ++q) nrm2 = nrm2 + dv[q] * dv[q];
+      for (int t = 0; t < kDescLen; ++t) nrm2 = nrm2 + dv[t] * dv[t];
       const float sq = sqrtf(nrm2);
-      bc[wv][1] = 512.f / (sq < FLT_EPSILON ? FLT_EPSILON : sq);
+      bc[g][1] = 512.f / (sq < FLT_EPSILON ? FLT_EPSILON : sq);
     }
     wave_sync_d();
-    const float nrm2s = bc[wv][1];
-    for (int q = lane; q < kDescLen; q += 64) dv[q] = sat_u8(dv[q] * nrm2s) * nrm2s;
+    const float nrm2s = bc[g][1];
+    for (int t = q; t < kDescLen; t += 8) dv[t] = sat_u8(dv[t] * nrm2s) * nrm2s;
     wave_sync_d();
-    if (lane == 0) {
+    if (q == 0) {
       float nrm1 = 0;
-      for (int q = 0; q < kDescLen; ++q) nrm1 = nrm1 + dv[q];
-      bc[wv][2] = 1.f / (nrm1 < FLT_EPSILON ? FLT_EPSILON : nrm1);
+      for (int t = 0; t < kDescLen; ++t) nrm1 = nrm1 + dv[t];
+      bc[g][2] = 1.f / (nrm1 < FLT_EPSILON ? FLT_EPSILON : nrm1);
     }
     wave_sync_d();
-    const float nrm1 = bc[wv][2];
-    float* out = A.desc + (long long)k * kDescLen;
-    for (int q = lane; q < kDescLen; q += 64) out[q] = sqrtf(dv[q] * nrm1);
+    const float nrm1 = bc[g][2];
+    if (active) {
+      float4* out = reinterpret_cast<float4*>(A.desc + (long long)k * kDescLen) + q * 4;
+      const float4* src = reinterpret_cast<const float4*>(dv) + q * 4;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 x = src[t];
+        out[t] = make_float4(sqrtf(x.x * nrm1), sqrtf(x.y * nrm1), sqrtf(x.z * nrm1), sqrtf(x.w * nrm1));
+      }
+    }
     wave_sync_d();
   }
 }
@@ -233,12 +330,12 @@ void launch_math_selftest(hipStream_t st, int op, const float* a, const float* b
                      mc);
 }
 
-void launch_descriptors(hipStream_t st, const Layout& L, const float* gpyr, const MathConsts* mc,
+void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, const MathConsts* mc,
                         const sift_keypoint* kpts, const int* img_kp_off, int batch, int kp_cap,
                         float* desc, int first_octave, int* err_flag) {
   DescArgs A;
   A.L = L;
-  A.gpyr = gpyr;
+  A.grad = grad;
   A.mc = mc;
   A.kpts = kpts;
   A.img_kp_off = img_kp_off;
@@ -247,7 +344,7 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float* gpyr, cons
   A.desc = desc;
   A.first_octave = first_octave;
   A.err_flag = err_flag;
-  hipLaunchKernelGGL(descriptor_kernel, dim3(2048), dim3(256), 0, st, A);
+  hipLaunchKernelGGL(descriptor_kernel, dim3(8192), dim3(64), 0, st, A);
 }
 
 }  // namespace sift

@@ -4,12 +4,15 @@
 // Output order must equal the reference's: octave -> layer -> row -> col ->
 // histogram peak (src/sift.cpp:556-557, 487-491, 525), duplicates kept.  The
 // GPU therefore never appends with atomics:
-//   extrema_count  -- one 256-lane workgroup per 2048 consecutive scan
-//                     positions of one image (positions enumerated in the
-//                     reference order), writes its candidate count;
-//   scan           -- exclusive scan of those counts (ordered offsets);
-//   extrema_write  -- recomputes the 26-neighbour test and writes candidates
-//                     at ballot-ranked positions: the list comes out sorted;
+//   dog_extrema    -- one workgroup per 64x16 tile of one octave: the four
+//                     DoG planes (+1-pixel halo) are formed in LDS from the
+//                     five Gaussian planes (and written out), then both
+//                     detection layers are tested from LDS; each wave row is
+//                     one ballot -> two 32-bit words of a candidate bitmask;
+//   mask_count / scan / mask_expand -- the bitmask's word order is the
+//                     reference's (octave, layer, row, col) order, so an
+//                     exclusive scan of per-chunk popcounts gives every
+//                     candidate its slot: the list comes out sorted;
 //   refine_orient  -- one wave per candidate: adjustLocalExtrema redundantly
 //                     on every lane (uniform control, broadcast loads), then
 //                     the 36-bin orientation histogram with per-sample work
@@ -32,86 +35,83 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ---- scan segments: (octave, layer) interiors in reference order ----------
-constexpr int kChunk = 2048;  // scan positions per workgroup
+// ---- candidate bitmask: one bit per (octave, layer, row, col) -------------
+// Plane (o, layer) holds rows x wpr 32-bit words (wpr = ceil(cols/32)), bit c%32
+// of word r*wpr + c/32; planes follow in (o, layer) order.  Word order within an
+// image is therefore exactly the reference's scan order (src/sift.cpp:556-557,
+// 487-491), which makes the ordered compaction a plain scan over words.
 constexpr int kMaxSeg = 2 * kMaxOctaves;
+constexpr int kWordChunk = 2048;  // mask words per workgroup in the count/expand passes
 
-struct SegTable {
-  int n;
-  int bpi;                        // workgroups per image
-  long long total;                // scan positions per image
-  long long start[kMaxSeg + 1];   // first position of each segment
-  int o[kMaxSeg], layer[kMaxSeg], w[kMaxSeg];
-  long long d_off[kMaxSeg];       // DoG plane offset of the segment's layer
-  long long plane[kMaxSeg];       // elements between consecutive DoG planes
-  int pitch[kMaxSeg];
-  long long d_img;
+struct MaskLayout {
+  int n;                          // segments = n_oct * 2
+  int bpw;                        // count/expand workgroups per image
+  long long w_img;                // words per image
+  long long start[kMaxSeg + 1];
+  int o[kMaxSeg], layer[kMaxSeg], wpr[kMaxSeg];
 };
 
-static SegTable make_segs(const Layout& L) {
-  SegTable S{};
+static MaskLayout make_mask(const Layout& L) {
+  MaskLayout M{};
   long long t = 0;
   int n = 0;
   for (int o = 0; o < L.n_oct; ++o)
     for (int layer = 1; layer <= kLayers; ++layer) {
-      const Octave& O = L.oct[o];
-      const int hr = O.rows - 2 * kBorder, wc = O.cols - 2 * kBorder;
-      S.start[n] = t;
-      S.o[n] = o;
-      S.layer[n] = layer;
-      S.w[n] = wc > 0 ? wc : 0;
-      S.d_off[n] = O.d_off[layer];
-      S.plane[n] = (long long)O.rows * O.pitch;
-      S.pitch[n] = O.pitch;
-      if (hr > 0 && wc > 0) t += (long long)hr * wc;
+      M.start[n] = t;
+      M.o[n] = o;
+      M.layer[n] = layer;
+      M.wpr[n] = (L.oct[o].cols + 31) / 32;
+      t += (long long)L.oct[o].rows * M.wpr[n];
       ++n;
     }
-  S.start[n] = t;
-  S.n = n;
-  S.total = t;
-  S.bpi = (int)((t + kChunk - 1) / kChunk);
-  if (S.bpi == 0) S.bpi = 1;
-  S.d_img = L.d_img;
-  return S;
+  M.start[n] = t;
+  M.n = n;
+  M.w_img = t;
+  M.bpw = (int)((t + kWordChunk - 1) / kWordChunk);
+  if (M.bpw == 0) M.bpw = 1;
+  return M;
 }
 
-int extrema_blocks_per_image(const Layout& L) { return make_segs(L).bpi; }
+long long mask_words_per_image(const Layout& L) { return make_mask(L).w_img; }
+int mask_blocks_per_image(const Layout& L) { return make_mask(L).bpw; }
 
-// Test of src/sift.cpp:493-511 at scan position g of image b.
-__device__ __forceinline__ bool extremum_at(const SegTable& S, const float* __restrict__ dog, int b,
-                                            long long g, int* seg_out, int* r_out, int* c_out) {
-  int s = 0;
-  while (s + 1 < S.n && S.start[s + 1] <= g) ++s;
-  const long long loc = g - S.start[s];
-  const int w = S.w[s];
-  const int r = kBorder + (int)(loc / w), c = kBorder + (int)(loc % w);
-  *seg_out = s;
-  *r_out = r;
-  *c_out = c;
-  const long long pitch = S.pitch[s];
-  const float* cur = dog + b * S.d_img + S.d_off[s] + r * pitch + c;
-  const float v = cur[0];
+// ---- pass 1: DoG (src/sift.cpp:280) fused with the 26-neighbour test --------
+constexpr int kExTW = 64, kExTH = 16;
+
+struct TileArgs {
+  Layout L;
+  MaskLayout M;
+  const float* gpyr;
+  float* dog;
+  float2* grad;      // (magnitude, fastAtan2 orientation) of Gaussian layers 1, 2
+  const MathConsts* mc;
+  unsigned* mask;
+  int tile_start[kMaxOctaves + 1];
+  int tiles_x[kMaxOctaves];
+  int write_dog;  // 1: form DoG from the Gaussian planes and write it; 0: read the DoG planes
+};
+
+// src/sift.cpp:493-511 on an LDS tile: v at (y, x) of plane cur; ties pass.
+__device__ __forceinline__ bool lds_extremum(const float (*lo)[kExTW + 4], const float (*cu)[kExTW + 4],
+                                             const float (*hi)[kExTW + 4], int y, int x) {
+  const float v = cu[y][x];
   if (!(fabsf(v) > kDogThreshold)) return false;
-  const float* prv = cur - S.plane[s];
-  const float* nxt = cur + S.plane[s];
   bool ok = true;
   if (v > 0) {
 #pragma unroll
     for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
       for (int dx = -1; dx <= 1; ++dx) {
-        const long long q = dy * pitch + dx;
-        ok = ok && v >= prv[q] && v >= nxt[q];
-        if (dy != 0 || dx != 0) ok = ok && v >= cur[q];
+        ok = ok && v >= lo[y + dy][x + dx] && v >= hi[y + dy][x + dx];
+        if (dy != 0 || dx != 0) ok = ok && v >= cu[y + dy][x + dx];
       }
   } else if (v < 0) {
 #pragma unroll
     for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
       for (int dx = -1; dx <= 1; ++dx) {
-        const long long q = dy * pitch + dx;
-        ok = ok && v <= prv[q] && v <= nxt[q];
-        if (dy != 0 || dx != 0) ok = ok && v <= cur[q];
+        ok = ok && v <= lo[y + dy][x + dx] && v <= hi[y + dy][x + dx];
+        if (dy != 0 || dx != 0) ok = ok && v <= cu[y + dy][x + dx];
       }
   } else {
     ok = false;
@@ -119,46 +119,151 @@ __device__ __forceinline__ bool extremum_at(const SegTable& S, const float* __re
   return ok;
 }
 
-__global__ __launch_bounds__(256) void extrema_count_kernel(SegTable S, const float* __restrict__ dog,
-                                                            int* __restrict__ blk_counts) {
+__global__ __launch_bounds__(256) void dog_extrema_kernel(TileArgs A) {
+  __shared__ float sd[kDogPer][kExTH + 2][kExTW + 4];
+  __shared__ float sg[2][kExTH + 2][kExTW + 4];  // Gaussian layers 1, 2 (for gradients)
+  const int b = blockIdx.y;
+  const int t = blockIdx.x;
+  int o = 0;
+  while (o + 1 < A.L.n_oct && A.tile_start[o + 1] <= t) ++o;
+  const int local = t - A.tile_start[o];
+  const int y0 = (local / A.tiles_x[o]) * kExTH, x0 = (local % A.tiles_x[o]) * kExTW;
+  const Octave& O = A.L.oct[o];
+  const long long pitch = O.pitch;
+  const float* g = A.gpyr + b * A.L.g_img;
+  float* dg = A.dog + b * A.L.d_img;
+  // DoG tile with a one-pixel halo, computed from the five Gaussian planes
+  // (or read, when the caller supplied the DoG pyramid)
+  for (int i = threadIdx.x; i < (kExTH + 2) * (kExTW + 2); i += 256) {
+    const int rr = i / (kExTW + 2), cc = i % (kExTW + 2);
+    const int y = y0 - 1 + rr, x = x0 - 1 + cc;
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f, g1 = 0.f, g2 = 0.f;
+    if (y >= 0 && y < O.rows && x >= 0 && x < O.cols) {
+      const long long p = (long long)y * pitch + x;
+      g1 = g[O.g_off[1] + p];
+      g2 = g[O.g_off[2] + p];
+      if (A.write_dog) {
+        const float g0 = g[O.g_off[0] + p], g3 = g[O.g_off[3] + p], g4 = g[O.g_off[4] + p];
+        d0 = g1 - g0;
+        d1 = g2 - g1;
+        d2 = g3 - g2;
+        d3 = g4 - g3;
+        if (rr >= 1 && rr <= kExTH && cc >= 1 && cc <= kExTW) {
+          dg[O.d_off[0] + p] = d0;
+          dg[O.d_off[1] + p] = d1;
+          dg[O.d_off[2] + p] = d2;
+          dg[O.d_off[3] + p] = d3;
+        }
+      } else {
+        d0 = dg[O.d_off[0] + p];
+        d1 = dg[O.d_off[1] + p];
+        d2 = dg[O.d_off[2] + p];
+        d3 = dg[O.d_off[3] + p];
+      }
+    }
+    sd[0][rr][cc] = d0;
+    sd[1][rr][cc] = d1;
+    sd[2][rr][cc] = d2;
+    sd[3][rr][cc] = d3;
+    sg[0][rr][cc] = g1;
+    sg[1][rr][cc] = g2;
+  }
+  __syncthreads();
+  // Per-pixel gradient of layers 1 and 2 -- the (magnitude, orientation) that
+  // calcOrientationHist (src/sift.cpp:413-426) and calcSIFTDescriptor
+  // (:623-633) evaluate per window sample; both depend on the pixel only.
+  {
+    const AtanConsts ak = A.mc->t;
+    float2* gr = A.grad + b * A.L.g_img;
+    for (int i = threadIdx.x; i < 2 * kExTH * kExTW; i += 256) {
+      const int ls = i / (kExTH * kExTW), rem = i % (kExTH * kExTW);
+      const int rr = rem / kExTW, cc = rem % kExTW;
+      const int y = y0 + rr, x = x0 + cc;
+      if (y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1) {
+        const float(*G)[kExTW + 4] = sg[ls];
+        const float dx = (float)(G[rr + 1][cc + 2] - G[rr + 1][cc]);
+        const float dy = (float)(G[rr][cc + 1] - G[rr + 2][cc + 1]);
+        gr[O.g_off[1 + ls] + (long long)y * pitch + x] = make_float2(magnitude(dx, dy), fast_atan2(dy, dx, ak));
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int seg1 = 2 * o, seg2 = 2 * o + 1;
+  const int wpr = A.M.wpr[seg1];
+  for (int rr = wv; rr < kExTH; rr += 4) {
+    const int r = y0 + rr, c = x0 + lane;
+    const bool inside = r >= kBorder && r < O.rows - kBorder && c >= kBorder && c < O.cols - kBorder;
+    const bool f1 = inside && lds_extremum(sd[0], sd[1], sd[2], rr + 1, lane + 1);
+    const bool f2 = inside && lds_extremum(sd[1], sd[2], sd[3], rr + 1, lane + 1);
+    const unsigned long long m1 = __ballot(f1), m2 = __ballot(f2);
+    if (r < O.rows && (lane == 0 || lane == 32)) {
+      const int w = x0 / 32 + (lane >> 5);
+      if (w < wpr) {
+        const long long base = b * A.M.w_img + (long long)r * wpr + w;
+        A.mask[base + A.M.start[seg1]] = (unsigned)(m1 >> lane);
+        A.mask[base + A.M.start[seg2]] = (unsigned)(m2 >> lane);
+      }
+    }
+  }
+}
+
+// ---- pass 2: ordered compaction of the bitmask ----------------------------
+__global__ __launch_bounds__(256) void mask_count_kernel(const unsigned* __restrict__ mask, long long w_img,
+                                                         int bpw, int* __restrict__ blk_counts) {
   __shared__ int wsum[4];
   const int b = blockIdx.y;
-  const long long base = (long long)blockIdx.x * kChunk;
+  const long long base = (long long)blockIdx.x * kWordChunk;
+  const unsigned* m = mask + b * w_img;
   int cnt = 0;
-  for (int it = 0; it < kChunk / 256; ++it) {
-    const long long g = base + it * 256 + threadIdx.x;
-    int sg, r, c;
-    if (g < S.total && extremum_at(S, dog, b, g, &sg, &r, &c)) ++cnt;
+#pragma unroll
+  for (int it = 0; it < kWordChunk / 256; ++it) {
+    const long long w = base + it * 256 + threadIdx.x;
+    if (w < w_img) cnt += __popc(m[w]);
   }
-  // wave reduce then block reduce (integer: order-free)
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
   __syncthreads();
-  if (threadIdx.x == 0) blk_counts[b * S.bpi + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (threadIdx.x == 0) blk_counts[b * bpw + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
-__global__ __launch_bounds__(256) void extrema_write_kernel(SegTable S, const float* __restrict__ dog,
-                                                            const int* __restrict__ blk_off,
-                                                            Cand* __restrict__ cands, int cap) {
+__global__ __launch_bounds__(256) void mask_expand_kernel(MaskLayout M, const unsigned* __restrict__ mask,
+                                                          const int* __restrict__ blk_off,
+                                                          Cand* __restrict__ cands, int cap) {
   __shared__ int wcnt[4];
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long long base = (long long)blockIdx.x * kChunk;
-  int run = blk_off[b * S.bpi + blockIdx.x];
-  for (int it = 0; it < kChunk / 256; ++it) {
-    const long long g = base + it * 256 + threadIdx.x;
-    int sg = 0, r = 0, c = 0;
-    const bool f = g < S.total && extremum_at(S, dog, b, g, &sg, &r, &c);
-    const unsigned long long m = __ballot(f);
-    if (lane == 0) wcnt[wv] = __popcll(m);
+  const long long base = (long long)blockIdx.x * kWordChunk;
+  const unsigned* m = mask + b * M.w_img;
+  int run = blk_off[b * M.bpw + blockIdx.x];
+  for (int it = 0; it < kWordChunk / 256; ++it) {
+    const long long w = base + it * 256 + threadIdx.x;
+    unsigned bits = w < M.w_img ? m[w] : 0u;
+    const int cnt = __popc(bits);
+    int incl = cnt;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int tt = __shfl_up(incl, off);
+      if (lane >= off) incl += tt;
+    }
+    if (lane == 63) wcnt[wv] = incl;
     __syncthreads();
     int before = 0;
     for (int k = 0; k < wv; ++k) before += wcnt[k];
     const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-    if (f) {
-      const unsigned long long lt = (lane == 0) ? 0ull : (m & (~0ull >> (64 - lane)));
-      const int pos = run + before + __popcll(lt);
-      if (pos < cap) cands[pos] = Cand{b, S.o[sg] | (S.layer[sg] << 8), r, c};
+    if (bits) {
+      int s = 0;
+      while (s + 1 < M.n && M.start[s + 1] <= w) ++s;
+      const long long wi = w - M.start[s];
+      const int r = (int)(wi / M.wpr[s]);
+      const int c0 = (int)(wi % M.wpr[s]) * 32;
+      int pos = run + before + incl - cnt;
+      const int ol = M.o[s] | (M.layer[s] << 8);
+      while (bits) {
+        const int bit = __builtin_ctz(bits);
+        bits &= bits - 1;
+        if (pos < cap) cands[pos] = Cand{b, ol, r, c0 + bit};
+        ++pos;
+      }
     }
     run += tot;
     __syncthreads();
@@ -232,23 +337,70 @@ __global__ void gather_offsets_kernel(const int* __restrict__ scan, const int* _
   }
 }
 
-void launch_extrema(hipStream_t st, const Layout& L, const float* dog, int batch, DetectBufs& D) {
-  SegTable S = make_segs(L);
-  dim3 grid(S.bpi, batch);
-  hipLaunchKernelGGL(extrema_count_kernel, grid, dim3(256), 0, st, S, dog, D.blk_counts);
-  const int nblk = S.bpi * batch;
+// Standalone gradient planes for scales [s_lo, s_hi] (sub-module entry points
+// whose pyramids come from the caller).
+__global__ __launch_bounds__(256) void grad_kernel(const float* __restrict__ gpyr, float2* __restrict__ grad,
+                                                   long long g_img, long long g_off, int pitch, int rows,
+                                                   int cols, int nscale, long long plane,
+                                                   const MathConsts* __restrict__ mc) {
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int b = blockIdx.z / nscale, s = blockIdx.z % nscale;
+  if (!(y > 0 && y < rows - 1 && x > 0 && x < cols - 1)) return;
+  const long long off = b * g_img + g_off + s * plane + (long long)y * pitch + x;
+  const float* p = gpyr + off;
+  const float dx = (float)(p[1] - p[-1]);
+  const float dy = (float)(p[-pitch] - p[pitch]);
+  grad[off] = make_float2(magnitude(dx, dy), fast_atan2(dy, dx, mc->t));
+}
+
+void launch_grad(hipStream_t st, const Layout& L, const float* gpyr, float2* grad, int batch, int s_lo,
+                 int s_hi, const MathConsts* mc) {
+  for (int o = 0; o < L.n_oct; ++o) {
+    const Octave& O = L.oct[o];
+    const int ns = s_hi - s_lo + 1;
+    dim3 grid((O.cols + 63) / 64, (O.rows + 3) / 4, batch * ns);
+    hipLaunchKernelGGL(grad_kernel, grid, dim3(256), 0, st, gpyr, grad, L.g_img, O.g_off[s_lo], O.pitch,
+                       O.rows, O.cols, ns, (long long)O.rows * O.pitch, mc);
+  }
+}
+
+void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* dog, bool write_dog,
+                    float2* grad, const MathConsts* mc, int batch, DetectBufs& D) {
+  TileArgs A;
+  A.L = L;
+  A.M = make_mask(L);
+  A.gpyr = gpyr;
+  A.dog = dog;
+  A.grad = grad;
+  A.mc = mc;
+  A.mask = D.mask;
+  A.write_dog = write_dog ? 1 : 0;
+  int t = 0;
+  for (int o = 0; o < L.n_oct; ++o) {
+    A.tile_start[o] = t;
+    A.tiles_x[o] = (L.oct[o].cols + kExTW - 1) / kExTW;
+    t += A.tiles_x[o] * ((L.oct[o].rows + kExTH - 1) / kExTH);
+  }
+  A.tile_start[L.n_oct] = t;
+  hipLaunchKernelGGL(dog_extrema_kernel, dim3(t, batch), dim3(256), 0, st, A);
+  const MaskLayout& M = A.M;
+  hipLaunchKernelGGL(mask_count_kernel, dim3(M.bpw, batch), dim3(256), 0, st, D.mask, M.w_img, M.bpw,
+                     D.blk_counts);
+  const int nblk = M.bpw * batch;
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, D.blk_counts, 1, D.scan_tmp, nullptr,
                      nblk, nblk, D.cand_total);
-  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(128), 0, st, D.scan_tmp, nullptr, S.bpi,
+  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(128), 0, st, D.scan_tmp, nullptr, M.bpw,
                      batch, nullptr, 0, D.img_cand_off);
-  hipLaunchKernelGGL(extrema_write_kernel, grid, dim3(256), 0, st, S, dog, D.scan_tmp, D.cands,
-                     D.cand_cap);
+  hipLaunchKernelGGL(mask_expand_kernel, dim3(M.bpw, batch), dim3(256), 0, st, M, D.mask, D.scan_tmp,
+                     D.cands, D.cand_cap);
 }
 
 // ---- adjustLocalExtrema + calcOrientationHist + peaks ----------------------
 struct RefArgs {
   Layout L;
   const float* gpyr;
+  const float2* grad;
   const float* dog;
   const MathConsts* mc;
   const Cand* cands;
@@ -258,203 +410,254 @@ struct RefArgs {
   int* npeaks;
 };
 
-constexpr int kOriMaxSamples = 35 * 35;  // radius <= 17 (scl_octv <= 3.81)
+// adjustLocalExtrema (src/sift.cpp:287-388) for one candidate; every lane of
+// a group evaluates it redundantly (uniform control, broadcast loads).
+struct Refined {
+  bool ok;
+  int layer, r, c, octave;
+  float x, y, size, response;
+};
 
-__global__ __launch_bounds__(256) void refine_orient_kernel(RefArgs A) {
-  __shared__ int sbin[4][kOriMaxSamples + 3];
-  __shared__ float sval[4][kOriMaxSamples + 3];
-  __shared__ float sh[4][kOriBins + 4];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+__device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const float* __restrict__ dimg,
+                                                    int o, int layer, int r, int c) {
+  const Octave& O = Lay.oct[o];
+  const long long pitch = O.pitch;
+  const float img_scale = 1. / 255;
+  const float deriv_scale = img_scale * 0.5f;
+  const float second_scale = img_scale;
+  const float cross_scale = img_scale * 0.25f;
+  float xi = 0, xr = 0, xc = 0, contr = 0;
+  Refined R{};
+  R.ok = true;
+  int it = 0;
+#define AT(pl, yy, xx) ((pl)[(long long)(yy)*pitch + (xx)])
+  for (; it < kMaxInterp; ++it) {
+    const float* cur = dimg + O.d_off[layer];
+    const float* lo = dimg + O.d_off[layer - 1];
+    const float* hi = dimg + O.d_off[layer + 1];
+    const float g[3] = {(AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale,
+                        (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale,
+                        (AT(hi, r, c) - AT(lo, r, c)) * deriv_scale};
+    const float v2 = (float)AT(cur, r, c) * 2;
+    const float dxx = (AT(cur, r, c + 1) + AT(cur, r, c - 1) - v2) * second_scale;
+    const float dyy = (AT(cur, r + 1, c) + AT(cur, r - 1, c) - v2) * second_scale;
+    const float dss = (AT(hi, r, c) + AT(lo, r, c) - v2) * second_scale;
+    const float dxy = (AT(cur, r + 1, c + 1) - AT(cur, r + 1, c - 1) - AT(cur, r - 1, c + 1) +
+                       AT(cur, r - 1, c - 1)) * cross_scale;
+    const float dxs = (AT(hi, r, c + 1) - AT(hi, r, c - 1) - AT(lo, r, c + 1) + AT(lo, r, c - 1)) *
+                      cross_scale;
+    const float dys = (AT(hi, r + 1, c) - AT(hi, r - 1, c) - AT(lo, r + 1, c) + AT(lo, r - 1, c)) *
+                      cross_scale;
+    const float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
+    float X[3];
+    solve3(H, g, X);
+    xi = -X[2];
+    xr = -X[1];
+    xc = -X[0];
+    if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+    if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) ||
+        fabsf(xc) > (float)(INT_MAX / 3)) {
+      R.ok = false;
+      return R;
+    }
+    c += cv_round(xc);
+    r += cv_round(xr);
+    layer += cv_round(xi);
+    if (layer < 1 || layer > kLayers || c < kBorder || c >= O.cols - kBorder || r < kBorder ||
+        r >= O.rows - kBorder) {
+      R.ok = false;
+      return R;
+    }
+  }
+  if (it >= kMaxInterp) {
+    R.ok = false;
+    return R;
+  }
+  {
+    const float* cur = dimg + O.d_off[layer];
+    const float* lo = dimg + O.d_off[layer - 1];
+    const float* hi = dimg + O.d_off[layer + 1];
+    const float g0 = (AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale;
+    const float g1 = (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale;
+    const float g2 = (AT(hi, r, c) - AT(lo, r, c)) * deriv_scale;
+    float t = 0;  // Matx::dot: s = 0; s += a_i * b_i
+    t = t + g0 * xc;
+    t = t + g1 * xr;
+    t = t + g2 * xi;
+    contr = AT(cur, r, c) * img_scale + t * 0.5f;
+    if (fabsf(contr) * kLayers < (float)0.04) {
+      R.ok = false;
+      return R;
+    }
+    const float v2 = AT(cur, r, c) * 2.f;
+    const float dxx = (AT(cur, r, c + 1) + AT(cur, r, c - 1) - v2) * second_scale;
+    const float dyy = (AT(cur, r + 1, c) + AT(cur, r - 1, c) - v2) * second_scale;
+    const float dxy = (AT(cur, r + 1, c + 1) - AT(cur, r + 1, c - 1) - AT(cur, r - 1, c + 1) +
+                       AT(cur, r - 1, c - 1)) * cross_scale;
+    const float tr = dxx + dyy;
+    const float det = dxx * dyy - dxy * dxy;
+    const float et = 10.f;
+    if (det <= 0 || tr * tr * et >= (et + 1) * (et + 1) * det) {
+      R.ok = false;
+      return R;
+    }
+  }
+#undef AT
+  R.layer = layer;
+  R.r = r;
+  R.c = c;
+  R.x = (c + xc) * (1 << o);
+  R.y = (r + xr) * (1 << o);
+  R.octave = o + (layer << 8) + (cv_round_d((xi + 0.5) * 255) << 16);
+  R.size = (float)kSigma * pow2f_cr((layer + xi) / kLayers) * (1 << o) * 2;
+  R.response = fabsf(contr);
+  return R;
+}
+
+// Eight candidates per wave (lanes 8g..8g+7 own candidate g).  Orientation
+// samples are computed 8 at a time per group and added to the group's 36-bin
+// histogram in raster order, lane q of the group at step q (ds_add_f32; one
+// instruction advances all eight groups' ordered chains).
+constexpr int kOGrp = 8;
+
+__device__ __forceinline__ void ohist_add(float* p, float v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+__global__ __launch_bounds__(64) void refine_orient_kernel(RefArgs A) {
+  __shared__ float oh[kOGrp][kOriBins + 4];
+  __shared__ float sm[kOGrp][kOriBins + 4];
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 3, q = lane & 7;
   int n = *A.cand_total;
   if (n > A.cand_cap) n = A.cand_cap;
   const ExpConsts ek = A.mc->e;
-  const AtanConsts ak = A.mc->t;
-  const float* etab = A.mc->exptab;
+  __shared__ float etab[64];  // exp32f table, LDS-resident (gathered per sample)
+  etab[lane] = A.mc->exptab[lane];
+  wave_sync();
 
-  for (int ci = blockIdx.x * 4 + wv; ci < n; ci += gridDim.x * 4) {
-    const Cand cd = A.cands[ci];
+  // XCD-aware contiguous split of the raster-ordered candidates (speed only)
+  const int xcd = blockIdx.x & 7, nslot = gridDim.x >> 3, slot = blockIdx.x >> 3;
+  const int per = ((n + 7) / 8 + kOGrp - 1) / kOGrp * kOGrp;
+  const int cend = min(n, (xcd + 1) * per);
+  for (int cb = xcd * per + slot * kOGrp; cb < cend; cb += nslot * kOGrp) {
+    const int ci = cb + g;
+    Refined R{};
+    Cand cd{0, 0, 0, 0};
+    if (ci < cend) {
+      cd = A.cands[ci];
+      R = refine_candidate(A.L, A.dog + cd.b * A.L.d_img, cd.ol & 255, cd.ol >> 8, cd.r, cd.c);
+    }
     const int o = cd.ol & 255;
-    int layer = cd.ol >> 8;
-    int r = cd.r, c = cd.c;
     const Octave& O = A.L.oct[o];
     const long long pitch = O.pitch;
-    const float* dimg = A.dog + cd.b * A.L.d_img;
-    // ---- adjustLocalExtrema, src/sift.cpp:287-388 (all lanes, uniform) ----
-    const float img_scale = 1. / 255;
-    const float deriv_scale = img_scale * 0.5f;
-    const float second_scale = img_scale;
-    const float cross_scale = img_scale * 0.25f;
-    float xi = 0, xr = 0, xc = 0, contr = 0;
-    bool ok = true;
-    int it = 0;
-#define AT(pl, yy, xx) ((pl)[(long long)(yy)*pitch + (xx)])
-    for (; it < kMaxInterp; ++it) {
-      const float* cur = dimg + O.d_off[layer];
-      const float* lo = dimg + O.d_off[layer - 1];
-      const float* hi = dimg + O.d_off[layer + 1];
-      const float g[3] = {(AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale,
-                          (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale,
-                          (AT(hi, r, c) - AT(lo, r, c)) * deriv_scale};
-      const float v2 = (float)AT(cur, r, c) * 2;
-      const float dxx = (AT(cur, r, c + 1) + AT(cur, r, c - 1) - v2) * second_scale;
-      const float dyy = (AT(cur, r + 1, c) + AT(cur, r - 1, c) - v2) * second_scale;
-      const float dss = (AT(hi, r, c) + AT(lo, r, c) - v2) * second_scale;
-      const float dxy = (AT(cur, r + 1, c + 1) - AT(cur, r + 1, c - 1) - AT(cur, r - 1, c + 1) +
-                         AT(cur, r - 1, c - 1)) * cross_scale;
-      const float dxs = (AT(hi, r, c + 1) - AT(hi, r, c - 1) - AT(lo, r, c + 1) + AT(lo, r, c - 1)) *
-                        cross_scale;
-      const float dys = (AT(hi, r + 1, c) - AT(hi, r - 1, c) - AT(lo, r + 1, c) + AT(lo, r - 1, c)) *
-                        cross_scale;
-      const float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
-      float X[3];
-      solve3(H, g, X);
-      xi = -X[2];
-      xr = -X[1];
-      xc = -X[0];
-      if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
-      if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) ||
-          fabsf(xc) > (float)(INT_MAX / 3)) {
-        ok = false;
-        break;
-      }
-      c += cv_round(xc);
-      r += cv_round(xr);
-      layer += cv_round(xi);
-      if (layer < 1 || layer > kLayers || c < kBorder || c >= O.cols - kBorder || r < kBorder ||
-          r >= O.rows - kBorder) {
-        ok = false;
-        break;
-      }
-    }
-    if (ok && it >= kMaxInterp) ok = false;
-    if (ok) {
-      const float* cur = dimg + O.d_off[layer];
-      const float* lo = dimg + O.d_off[layer - 1];
-      const float* hi = dimg + O.d_off[layer + 1];
-      const float g0 = (AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale;
-      const float g1 = (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale;
-      const float g2 = (AT(hi, r, c) - AT(lo, r, c)) * deriv_scale;
-      float t = 0;
-      t = t + g0 * xc;
-      t = t + g1 * xr;
-      t = t + g2 * xi;
-      contr = AT(cur, r, c) * img_scale + t * 0.5f;
-      if (fabsf(contr) * kLayers < (float)0.04) {
-        ok = false;
-      } else {
-        const float v2 = AT(cur, r, c) * 2.f;
-        const float dxx = (AT(cur, r, c + 1) + AT(cur, r, c - 1) - v2) * second_scale;
-        const float dyy = (AT(cur, r + 1, c) + AT(cur, r - 1, c) - v2) * second_scale;
-        const float dxy = (AT(cur, r + 1, c + 1) - AT(cur, r + 1, c - 1) - AT(cur, r - 1, c + 1) +
-                           AT(cur, r - 1, c - 1)) * cross_scale;
-        const float tr = dxx + dyy;
-        const float det = dxx * dyy - dxy * dxy;
-        const float et = 10.f;
-        if (det <= 0 || tr * tr * et >= (et + 1) * (et + 1) * det) ok = false;
-      }
-    }
-    if (!ok) {
-      if (lane == 0) A.npeaks[ci] = 0;
-      continue;
-    }
-    const float kx = (c + xc) * (1 << o);
-    const float ky = (r + xr) * (1 << o);
-    const int koct = o + (layer << 8) + (cv_round_d((xi + 0.5) * 255) << 16);
-    const float ksize = (float)kSigma * pow2f_cr((layer + xi) / kLayers) * (1 << o) * 2;
-    const float kresp = fabsf(contr);
-
     // ---- calcOrientationHist, src/sift.cpp:389-458 ----
-    const float scl = ksize * 0.5f / (1 << o);
-    const int radius = cv_round(3 * 1.5f * scl);
+    const float scl = R.size * 0.5f / (1 << o);
+    const int radius = R.ok ? cv_round(3 * 1.5f * scl) : 0;
     const float sigma = 1.5f * scl;
     const float escale = -1.f / (2.f * sigma * sigma);
-    const float* gimg = A.gpyr + cd.b * A.L.g_img + O.g_off[layer];
+    const float2* gimg = A.grad + cd.b * A.L.g_img + O.g_off[R.ok ? R.layer : 0];
     const int D = 2 * radius + 1;
-    const int ns = D * D;  // <= kOriMaxSamples
-    for (int s = lane; s < ns; s += 64) {
-      const int i = s / D - radius, j = s % D - radius;
-      const int y = r + i, x = c + j;
+    const int ns = R.ok ? D * D : 0;
+    for (int t = q; t < kOriBins; t += 8) oh[g][t] = 0.f;
+    int nmax = ns;
+    nmax = max(nmax, __shfl_xor(nmax, 8));
+    nmax = max(nmax, __shfl_xor(nmax, 16));
+    nmax = max(nmax, __shfl_xor(nmax, 32));
+    wave_sync();
+    for (int base = 0; base < nmax; base += 8) {
+      const int s = base + q;
       int bin = -1;
       float val = 0.f;
-      if (!(y <= 0 || y >= O.rows - 1) && !(x <= 0 || x >= O.cols - 1)) {
-        const float dx = (float)(AT(gimg, y, x + 1) - AT(gimg, y, x - 1));
-        const float dy = (float)(AT(gimg, y - 1, x) - AT(gimg, y + 1, x));
-        const float w = exp32f((i * i + j * j) * escale, etab, ek);
-        const float ori = fast_atan2(dy, dx, ak);
-        const float mag = magnitude(dx, dy);
-        bin = cv_round((kOriBins / 360.f) * ori);
-        if (bin >= kOriBins) bin -= kOriBins;
-        if (bin < 0) bin += kOriBins;
-        val = w * mag;
+      if (s < ns) {
+        const int i = s / D - radius, j = s % D - radius;
+        const int y = R.r + i, x = R.c + j;
+        if (!(y <= 0 || y >= O.rows - 1) && !(x <= 0 || x >= O.cols - 1)) {
+          const float2 mo = gimg[(long long)y * pitch + x];  // (Mag, Ori) of the pixel
+          const float w = exp32f((i * i + j * j) * escale, etab, ek);
+          const float ori = mo.y;
+          const float mag = mo.x;
+          bin = cv_round((kOriBins / 360.f) * ori);
+          if (bin >= kOriBins) bin -= kOriBins;
+          if (bin < 0) bin += kOriBins;
+          val = w * mag;
+        }
       }
-      sbin[wv][s] = bin;
-      sval[wv][s] = val;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj)
+        if (q == jj && bin >= 0) ohist_add(&oh[g][bin], val);
     }
     wave_sync();
-    // owner-computes: lane j accumulates bin j in sample (raster) order
-    float acc = 0.f;
-    if (lane < kOriBins) {
-      for (int s = 0; s < ns; ++s) {
-        const float v = sval[wv][s];
-        acc = acc + ((sbin[wv][s] == lane) ? v : 0.f);
-      }
-      sh[wv][lane] = acc;
+    // smoothing (src/sift.cpp:440-451), max, peaks (src/sift.cpp:524-541)
+    float mx = -1.f;
+    for (int t = q; t < kOriBins; t += 8) {
+      const float* th = oh[g];
+      const int jm2 = (t + kOriBins - 2) % kOriBins, jp2 = (t + 2) % kOriBins;
+      const int jm1 = (t + kOriBins - 1) % kOriBins, jp1 = (t + 1) % kOriBins;
+      const float h = (th[jm2] + th[jp2]) * (1.f / 16.f) + (th[jm1] + th[jp1]) * (4.f / 16.f) +
+                      th[t] * (6.f / 16.f);
+      sm[g][t] = h;
+      mx = fmaxf(mx, h);
     }
-    wave_sync();
-    float h = 0.f;
-    if (lane < kOriBins) {
-      const float* th = sh[wv];
-      const int jm2 = (lane + kOriBins - 2) % kOriBins, jp2 = (lane + 2) % kOriBins;
-      const int jm1 = (lane + kOriBins - 1) % kOriBins, jp1 = (lane + 1) % kOriBins;
-      h = (th[jm2] + th[jp2]) * (1.f / 16.f) + (th[jm1] + th[jp1]) * (4.f / 16.f) +
-          th[lane] * (6.f / 16.f);
-    }
-    float mx = lane < kOriBins ? h : -1.f;
-    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-    wave_sync();
-    if (lane < kOriBins) sh[wv][lane] = h;
+    mx = fmaxf(mx, __shfl_xor(mx, 1));
+    mx = fmaxf(mx, __shfl_xor(mx, 2));
+    mx = fmaxf(mx, __shfl_xor(mx, 4));
     wave_sync();
     const float mag_thr = (float)(mx * 0.8f);
-    bool peak = false;
-    float angle = 0.f;
-    if (lane < kOriBins) {
-      const int l = lane > 0 ? lane - 1 : kOriBins - 1;
-      const int rr = lane < kOriBins - 1 ? lane + 1 : 0;
-      const float hl = sh[wv][l], hr = sh[wv][rr];
-      if (h > hl && h > hr && h >= mag_thr) {
-        peak = true;
-        float bin = lane + 0.5f * (hl - hr) / (hl - 2 * h + hr);
-        bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
-        angle = 360.f - (float)((360.f / kOriBins) * bin);
-        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+    unsigned long long pmask = 0;
+    float ang[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      const int t = q + 8 * m;
+      ang[m] = 0.f;
+      if (t < kOriBins && R.ok) {
+        const int l = t > 0 ? t - 1 : kOriBins - 1;
+        const int rr = t < kOriBins - 1 ? t + 1 : 0;
+        const float h = sm[g][t], hl = sm[g][l], hr = sm[g][rr];
+        if (h > hl && h > hr && h >= mag_thr) {
+          float bin = t + 0.5f * (hl - hr) / (hl - 2 * h + hr);
+          bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
+          float a = 360.f - (float)((360.f / kOriBins) * bin);
+          if (fabsf(a - 360.f) < FLT_EPSILON) a = 0.f;
+          ang[m] = a;
+          pmask |= 1ull << t;
+        }
       }
     }
-    const unsigned long long pm = __ballot(peak);
-    CandOut* co = A.couts + ci;
-    if (peak) {
-      const unsigned long long lt = (lane == 0) ? 0ull : (pm & (~0ull >> (64 - lane)));
-      co->angle[__popcll(lt)] = angle;
-    }
-    if (lane == 0) {
-      co->x = kx;
-      co->y = ky;
-      co->size = ksize;
-      co->response = kresp;
-      co->octave = koct;
-      co->img = cd.b;
-      co->npeaks = __popcll(pm);
-      A.npeaks[ci] = __popcll(pm);
+    // OR-reduce the group's peak mask (lanes of a group own disjoint bins)
+    pmask |= __shfl_xor(pmask, 1);
+    pmask |= __shfl_xor(pmask, 2);
+    pmask |= __shfl_xor(pmask, 4);
+    if (ci < cend) {
+      CandOut* co = A.couts + ci;
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        const int t = q + 8 * m;
+        if (t < kOriBins && ((pmask >> t) & 1ull))
+          co->angle[__popcll(pmask & ((1ull << t) - 1ull))] = ang[m];
+      }
+      const int np = R.ok ? __popcll(pmask) : 0;
+      if (q == 0) {
+        co->x = R.x;
+        co->y = R.y;
+        co->size = R.size;
+        co->response = R.response;
+        co->octave = R.octave;
+        co->img = cd.b;
+        co->npeaks = np;
+        A.npeaks[ci] = np;
+      }
     }
     wave_sync();
-#undef AT
   }
 }
 
-void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, const float* dog,
-                          const MathConsts* mc, DetectBufs& D, int batch) {
+void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, const float2* grad,
+                          const float* dog, const MathConsts* mc, DetectBufs& D, int batch) {
   RefArgs A;
   A.L = L;
   A.gpyr = gpyr;
+  A.grad = grad;
   A.dog = dog;
   A.mc = mc;
   A.cands = D.cands;
@@ -463,7 +666,7 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.couts = D.couts;
   A.npeaks = D.npeaks;
   (void)batch;
-  hipLaunchKernelGGL(refine_orient_kernel, dim3(2048), dim3(256), 0, st, A);
+  hipLaunchKernelGGL(refine_orient_kernel, dim3(8192), dim3(64), 0, st, A);
 }
 
 // ---- ordered keypoint emission ------------------------------------------------
