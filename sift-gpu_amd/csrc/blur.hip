@@ -12,8 +12,9 @@
 //     its w-halo is staged once into LDS (zero-filled, so the padding rule is a
 //     branch-free read);
 //   * each lane owns PX consecutive outputs of one row and slides a register
-//     window of PX + 2w source values per kernel row (float4 LDS reads), so one
-//     LDS word feeds ~2w+1 multiply-adds;
+//     window of PX + 2w source values per kernel row (bank-conflict-free
+//     ds_read_b128, see lane_to_pixel), so one LDS word feeds ~2w+1
+//     multiply-adds;
 //   * kernel rows are uniform across the wave, so the 2w+1 coefficients of a
 //     row come from the scalar cache into SGPRs (VALU ops take them directly);
 //   * the four scales of an octave are blurred by ONE launch (blockIdx.z picks
@@ -49,16 +50,32 @@ constexpr int kTY = 32;   // tile rows (one lane row each)
 constexpr int kTX = 256 / kTY;
 constexpr int kTileW = kTX * kPX;
 
+// Window reads are ds_read_b128, whose wave64 access is served in four
+// 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32.  Lanes
+// are assigned to output pixels so that each group holds two whole tile rows
+// (ty, ty+1) x 8 lanes; with the LDS row pitch LP = 4 (mod 8) words the 16
+// lanes' 16-byte slots (ty*LP/4 + 2*tx + k) mod 16 are all distinct:
+// bank-conflict free.
+__device__ __forceinline__ void lane_to_pixel(int lane, int& ty, int& tx) {
+  const int l = lane & 31;
+  const bool g2 = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;  // group 2 of the half
+  // position of l inside its group (lanes listed in ascending order)
+  int pos;
+  if (!g2) pos = l < 4 ? l : l < 16 ? l - 8 : l - 12;      // 0-3, 12-15, 20-27
+  else pos = l < 12 ? l - 4 : l < 20 ? l - 8 : l - 16;     // 4-11, 16-19, 28-31
+  ty = ((lane >> 5) * 2 + (g2 ? 1 : 0)) * 2 + (pos >> 3);
+  tx = pos & 7;
+}
+
 template <int W>
 struct BlurTile {
   static constexpr int KS = 2 * W + 1;
   static constexpr int LW = kTileW + 2 * W;
-  static constexpr int LP0 = (LW + 3) & ~3;
-  static constexpr int LP = (LP0 % 8 == 0) ? LP0 + 4 : LP0;  // odd multiple of 4 words
+  static constexpr int LP = ((LW + 3) / 8) * 8 + 4;
   static constexpr int LR = kTY + 2 * W;
   static constexpr int LDS_FLOATS = LR * LP;
   static constexpr int NWIN = kPX + 2 * W;
-  static_assert(NWIN % 4 == 0, "window must be float4-readable (W even)");
+  static_assert(NWIN % 4 == 0 && LP % 8 == 4 && LP >= LW, "window layout");
 };
 
 template <int W>
@@ -79,7 +96,9 @@ __device__ __forceinline__ void blur_tile(const float* __restrict__ src, long lo
     }
   }
   __syncthreads();
-  const int tx = tid % kTX, ty = tid / kTX;
+  int tx, ty;
+  lane_to_pixel(lane, ty, tx);
+  ty += wv * 8;
   float acc[kPX];
 #pragma unroll
   for (int p = 0; p < kPX; ++p) acc[p] = 0.f;
