@@ -172,44 +172,50 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
         rlen = e >> 16;
       }
     }
-    for (int base = 0; base < nmax; base += 8) {
-      int pk = -1;
-      float v[8];
-      if (base + q < nsamp) {
-        const int i = ri - radius, j = rlo + u;
-        const float c_rot = j * cos_t - i * sin_t;
-        const float r_rot = j * sin_t + i * cos_t;
-        float rbin = r_rot + d / 2 - 0.5f;
-        float cbin = c_rot + d / 2 - 0.5f;
-        const int r = py + i, c = px + j;
-        if (rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 &&
-            c < cols - 1) {
-          const float2 mo = gimg[(long long)r * pitch + c];  // (Mag, Ori) of the pixel
-          const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab, ek);
-          float obin = (mo.y - ori) * bins_per_rad;
-          const float mag = mo.x * w;
-          const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
-          int o0 = cv_floor(obin);
-          rbin -= r0;
-          cbin -= c0;
-          obin -= o0;
-          if (o0 < 0) o0 += nb;
-          if (o0 >= nb) o0 -= nb;
-          const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-          const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-          const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-          v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
-          v[6] = v_rc11 - v[7];
-          v[5] = v_rc10 * obin;
-          v[4] = v_rc10 - v[5];
-          v[3] = v_rc01 * obin;
-          v[2] = v_rc01 - v[3];
-          v[1] = v_rc00 * obin;
-          v[0] = v_rc00 - v[1];
-          pk = (r0 + 1) | ((c0 + 1) << 4) | (o0 << 8);
-        }
-      }
-      u += 8;  // advance to candidate sample t + 8
+    // Software pipeline: each step stashes batch k, then computes batch k+1
+    // (independent VALU + one gather) in the same basic block as batch k's
+    // ordered LDS read-modify-write chain, so the scheduler fills the chain's
+    // LDS latency with the next batch's arithmetic.  Both halves are
+    // branch-free: an invalid sample adds +0.0f to bin 0 (exact no-op, every
+    // bin is >= +0) and gathers from a clamped in-plane address.
+    int pk_cur = -1;
+    float v_cur[8];
+    auto sample = [&](bool in_range, int& pk, float (&v)[8]) {
+      const int i = ri - radius, j = rlo + u;
+      const float c_rot = j * cos_t - i * sin_t;
+      const float r_rot = j * sin_t + i * cos_t;
+      float rbin = r_rot + d / 2 - 0.5f;
+      float cbin = c_rot + d / 2 - 0.5f;
+      const int r = py + i, c = px + j;
+      const bool ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 &&
+                      r < rows - 1 && c > 0 && c < cols - 1;
+      const int rcl = min(max(r, 0), rows - 1), ccl = min(max(c, 0), cols - 1);
+      const float2 mo = gimg[(long long)rcl * pitch + ccl];  // (Mag, Ori) of the pixel
+      const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab, ek);
+      float obin = (mo.y - ori) * bins_per_rad;
+      const float mag = mo.x * w;
+      const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
+      int o0 = cv_floor(obin);
+      rbin -= r0;
+      cbin -= c0;
+      obin -= o0;
+      if (o0 < 0) o0 += nb;
+      if (o0 >= nb) o0 -= nb;
+      const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+      const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+      const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+      v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
+      v[6] = v_rc11 - v[7];
+      v[5] = v_rc10 * obin;
+      v[4] = v_rc10 - v[5];
+      v[3] = v_rc01 * obin;
+      v[2] = v_rc01 - v[3];
+      v[1] = v_rc00 * obin;
+      v[0] = v_rc00 - v[1];
+      pk = ok ? (r0 + 1) | ((c0 + 1) << 4) | (o0 << 8) : -1;
+    };
+    auto advance = [&]() {  // to candidate sample t + 8
+      u += 8;
       while (ri < D && u >= rlen) {
         u -= rlen;
         if (++ri < D && table) {
@@ -218,26 +224,38 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
           rlen = e >> 16;
         }
       }
-      rbase[lane] = pk;
-      if (pk >= 0) {
-        float4* rv = reinterpret_cast<float4*>(rval + q * kRecStride + g * 8);
-        rv[0] = make_float4(v[0], v[1], v[2], v[3]);
-        rv[1] = make_float4(v[4], v[5], v[6], v[7]);
-      }
+    };
+    if (nmax > 0) {
+      sample(q < nsamp, pk_cur, v_cur);
+      advance();
+    }
+    for (int base = 0; base < nmax; base += 8) {
+      rbase[lane] = pk_cur;
+      float4* rv = reinterpret_cast<float4*>(rval + q * kRecStride + g * 8);
+      rv[0] = make_float4(v_cur[0], v_cur[1], v_cur[2], v_cur[3]);
+      rv[1] = make_float4(v_cur[4], v_cur[5], v_cur[6], v_cur[7]);
       wave_sync_d();
-      // ordered accumulation: lane q adds the corner of parity q of each sample
+      int pk_nxt;
+      float v_nxt[8];
+      sample(base + 8 + q < nsamp, pk_nxt, v_nxt);
+      // ordered accumulation of batch k: lane q adds the corner of parity q
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int p = rbase[g * 8 + jj];
-        if (p >= 0) {
-          const int R0 = p & 15, C0 = (p >> 4) & 15, O0 = p >> 8;
-          const int dr = ((q >> 2) ^ R0) & 1, dc = ((q >> 1) ^ C0) & 1, dO = (q ^ O0) & 1;
-          const float val = rval[jj * kRecStride + g * 8 + (dr * 4 + dc * 2 + dO)];
-          const int qi = ((R0 + dr) >> 1) * 15 + ((C0 + dc) >> 1) * 5 + ((O0 + dO) >> 1);
-          hist[qi * 64 + lane] = hist[qi * 64 + lane] + val;
-        }
+        const bool ok = p >= 0;
+        const int pp = ok ? p : 0;
+        const int R0 = pp & 15, C0 = (pp >> 4) & 15, O0 = pp >> 8;
+        const int dr = ((q >> 2) ^ R0) & 1, dc = ((q >> 1) ^ C0) & 1, dO = (q ^ O0) & 1;
+        const float rvv = rval[jj * kRecStride + g * 8 + (dr * 4 + dc * 2 + dO)];
+        const float val = ok ? rvv : 0.f;
+        const int qi = ((R0 + dr) >> 1) * 15 + ((C0 + dc) >> 1) * 5 + ((O0 + dO) >> 1);
+        hist[qi * 64 + lane] = hist[qi * 64 + lane] + val;
       }
       wave_sync_d();
+      advance();
+      pk_cur = pk_nxt;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v_cur[t] = v_nxt[t];
     }
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
     float cell[2][8];

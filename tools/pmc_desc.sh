@@ -1,1 +1,1 @@
-bash tools/pmc_kernel.sh "blur_octave" blur --batch 16
+bash tools/pmc_kernel.sh "descriptor" desc3 --batch 16
