@@ -35,7 +35,7 @@ __device__ __forceinline__ void wave_sync_d() {
 constexpr int kGrp = 8;            // keypoints per wave
 constexpr int kQBins = 45;         // bins per parity class: 3 x 3 x 5
 constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
-constexpr int kRecStride = 68;     // LDS row stride of the per-sample corner records
+constexpr int kRecStride2 = 132;   // words per sample row of the owner records (128 + pad)
 
 struct DescArgs {
   Layout L;
@@ -69,8 +69,9 @@ __device__ __forceinline__ void slab(float a, float b, int& lo, int& hi) {
 
 __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
-  __shared__ int rbase[kGrp * 8];                   // [group][sample]: r0+1 | (c0+1)<<4 | o0<<8
-  __shared__ __attribute__((aligned(16))) float rval[8 * kRecStride];  // [sample][group][corner]
+  // per-sample hand-off records: [sample j][group][owner q] = (bin address, value),
+  // row stride kRecStride2 words (conflict-free b128 stores, b64 loads)
+  __shared__ __attribute__((aligned(16))) float rec[8 * kRecStride2];
   __shared__ int rows_tab[kGrp][kMaxWinRows];       // per row: (jlo + 64) | len << 16
   __shared__ float bc[kGrp][4];
   __shared__ float etab[64];
@@ -176,11 +177,16 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
     // (independent VALU + one gather) in the same basic block as batch k's
     // ordered LDS read-modify-write chain, so the scheduler fills the chain's
     // LDS latency with the next batch's arithmetic.  Both halves are
-    // branch-free: an invalid sample adds +0.0f to bin 0 (exact no-op, every
-    // bin is >= +0) and gathers from a clamped in-plane address.
-    int pk_cur = -1;
-    float v_cur[8];
-    auto sample = [&](bool in_range, int& pk, float (&v)[8]) {
+    // branch-free: an invalid sample hands every owner "+0.0f into your bin 0"
+    // (exact no-op, every bin is >= +0) and gathers from a clamped address.
+    //
+    // The sample's lane resolves ownership for all 8 owners: with
+    // (R0, C0, O0) = (r0+1, c0+1, o0) and odd = parity bits of the base bin,
+    // owner q receives corner k = q ^ odd (so corner values are XOR-permuted by
+    // odd in three swap layers) into bin index
+    //   qi(q) = qi0 + [R0 odd and q_r = 0]*15 + [C0 odd and q_c = 0]*5 + [O0 odd and q_o = 0].
+    float4 rc_cur[4];  // (addr, val) x 8 owners of this lane's sample
+    auto sample = [&](bool in_range, float4 (&out)[4]) {
       const int i = ri - radius, j = rlo + u;
       const float c_rot = j * cos_t - i * sin_t;
       const float r_rot = j * sin_t + i * cos_t;
@@ -190,11 +196,13 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       const bool ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 &&
                       r < rows - 1 && c > 0 && c < cols - 1;
       const int rcl = min(max(r, 0), rows - 1), ccl = min(max(c, 0), cols - 1);
-      const float2 mo = gimg[(long long)rcl * pitch + ccl];  // (Mag, Ori) of the pixel
+      const float2 mo_raw = gimg[(long long)rcl * pitch + ccl];  // (Mag, Ori) of the pixel
+      // invalid: (0, 0) -- border gradients are never written and may hold NaN
+      const float2 mo = ok ? mo_raw : make_float2(0.f, 0.f);
       const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab, ek);
       float obin = (mo.y - ori) * bins_per_rad;
       const float mag = mo.x * w;
-      const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
+      int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
       int o0 = cv_floor(obin);
       rbin -= r0;
       cbin -= c0;
@@ -204,6 +212,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
       const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
       const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+      float v[8];
       v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
       v[6] = v_rc11 - v[7];
       v[5] = v_rc10 * obin;
@@ -212,7 +221,36 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       v[2] = v_rc01 - v[3];
       v[1] = v_rc00 * obin;
       v[0] = v_rc00 - v[1];
-      pk = ok ? (r0 + 1) | ((c0 + 1) << 4) | (o0 << 8) : -1;
+      const int R0 = ok ? r0 + 1 : 0, C0 = ok ? c0 + 1 : 0, O0 = ok ? o0 : 0;
+      const int odd = ((R0 & 1) << 2) | ((C0 & 1) << 1) | (O0 & 1);
+      // w[q] = v[q ^ odd]: three conditional swap layers
+#define SWAP_LAYER(bit, s)                                 \
+  if (odd & (bit)) {                                       \
+    _Pragma("unroll") for (int t = 0; t < 8; ++t) {        \
+      if (!(t & (bit))) {                                  \
+        const float x = v[t];                              \
+        v[t] = v[t + (s)];                                 \
+        v[t + (s)] = x;                                    \
+      }                                                    \
+    }                                                      \
+  }
+      SWAP_LAYER(1, 1)
+      SWAP_LAYER(2, 2)
+      SWAP_LAYER(4, 4)
+#undef SWAP_LAYER
+      const int base0 = ((R0 >> 1) * 15 + (C0 >> 1) * 5 + (O0 >> 1)) * 64 + g * 8;
+      const int t15 = (odd & 4) ? 15 * 64 : 0, t5 = (odd & 2) ? 5 * 64 : 0, t1 = (odd & 1) ? 64 : 0;
+#pragma unroll
+      for (int oq = 0; oq < 8; ++oq) {
+        const int addr = base0 + oq + ((oq & 4) ? 0 : t15) + ((oq & 2) ? 0 : t5) + ((oq & 1) ? 0 : t1);
+        if (oq & 1) {
+          out[oq >> 1].z = __int_as_float(addr);
+          out[oq >> 1].w = v[oq];
+        } else {
+          out[oq >> 1].x = __int_as_float(addr);
+          out[oq >> 1].y = v[oq];
+        }
+      }
     };
     auto advance = [&]() {  // to candidate sample t + 8
       u += 8;
@@ -226,36 +264,27 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       }
     };
     if (nmax > 0) {
-      sample(q < nsamp, pk_cur, v_cur);
+      sample(q < nsamp, rc_cur);
       advance();
     }
     for (int base = 0; base < nmax; base += 8) {
-      rbase[lane] = pk_cur;
-      float4* rv = reinterpret_cast<float4*>(rval + q * kRecStride + g * 8);
-      rv[0] = make_float4(v_cur[0], v_cur[1], v_cur[2], v_cur[3]);
-      rv[1] = make_float4(v_cur[4], v_cur[5], v_cur[6], v_cur[7]);
+      float4* dst4 = reinterpret_cast<float4*>(rec + q * kRecStride2 + g * 16);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dst4[t] = rc_cur[t];
       wave_sync_d();
-      int pk_nxt;
-      float v_nxt[8];
-      sample(base + 8 + q < nsamp, pk_nxt, v_nxt);
-      // ordered accumulation of batch k: lane q adds the corner of parity q
+      float4 rc_nxt[4];
+      sample(base + 8 + q < nsamp, rc_nxt);
+      // ordered accumulation of batch k: lane q applies its record of each sample
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
-        const int p = rbase[g * 8 + jj];
-        const bool ok = p >= 0;
-        const int pp = ok ? p : 0;
-        const int R0 = pp & 15, C0 = (pp >> 4) & 15, O0 = pp >> 8;
-        const int dr = ((q >> 2) ^ R0) & 1, dc = ((q >> 1) ^ C0) & 1, dO = (q ^ O0) & 1;
-        const float rvv = rval[jj * kRecStride + g * 8 + (dr * 4 + dc * 2 + dO)];
-        const float val = ok ? rvv : 0.f;
-        const int qi = ((R0 + dr) >> 1) * 15 + ((C0 + dc) >> 1) * 5 + ((O0 + dO) >> 1);
-        hist[qi * 64 + lane] = hist[qi * 64 + lane] + val;
+        const float2 e = reinterpret_cast<const float2*>(rec + jj * kRecStride2)[lane];
+        const int a = __float_as_int(e.x);
+        hist[a] = hist[a] + e.y;
       }
       wave_sync_d();
       advance();
-      pk_cur = pk_nxt;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v_cur[t] = v_nxt[t];
+      for (int t = 0; t < 4; ++t) rc_cur[t] = rc_nxt[t];
     }
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
     float cell[2][8];
