@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--octaves", type=int, default=5)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--no-fast", action="store_true", help="skip the SIFT_FLAG_FAST leg")
     p.add_argument("--profile-json", default=None, help="also write per-stage stats here")
     return p.parse_args()
 
@@ -97,33 +98,37 @@ def main():
         if world > 1 and not a.no_gather:
             sift_dist.gather_keypoints(kpts, offs, dst=0)
 
-    for _ in range(a.warmup):
-        step()
-    ctx.sync()  # checks device-side capacity flags
-    n_kp = int(offs[-1].item())
-    if n_kp > cap:
-        raise RuntimeError(f"keypoint capacity {cap} < {n_kp}")
-    ctx.stage_stats(reset=True)
+    def leg(flags):
+        """W warmup + K timed steps in one mode; returns (max-over-ranks seconds,
+        per-stage device stats of this rank, keypoints per step summed over ranks)."""
+        ctx.set_flags(flags)
+        for _ in range(a.warmup):
+            step()
+        ctx.sync()  # checks device-side capacity flags
+        n_kp = int(offs[-1].item())
+        if n_kp > cap:
+            raise RuntimeError(f"keypoint capacity {cap} < {n_kp}")
+        ctx.stage_stats(reset=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        stats = ctx.stage_stats(reset=True)
+        kp_step = torch.tensor([float(offs[-1].item())], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(kp_step, op=dist.ReduceOp.SUM)
+        return float(t.item()), stats, float(kp_step.item())
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    stats = ctx.stage_stats(reset=True)
-
-    kp_step = torch.tensor([float(offs[-1].item())], dtype=torch.float64, device="cuda")
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kp_step, op=dist.ReduceOp.SUM)
-    dt = float(t.item())
-    kp_total_step = float(kp_step.item())
+    dt, stats, kp_total_step = leg(siftgpu.SIFT_FLAG_PROFILE)
+    fast = None if a.no_fast else leg(siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
 
     if rank == 0:
         mpix = world * B * R * C * a.steps / 1e6
@@ -168,6 +173,26 @@ def main():
                         "note": "B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes), SURVEY.md 8(d)"},
             "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in stats.items()},
         }
+        if fast is not None:
+            fdt, fst, fkp = fast
+            pf = fst.get("pyramid_fast", {"ms": 0.0, "bytes": 0.0, "launches": 0})
+            gbs = pf["bytes"] / (pf["ms"] * 1e-3) / 1e9 if pf["ms"] else 0.0
+            out["fast_mode"] = {
+                "value": round(mpix / fdt, 2), "unit": "Mpix/s", "ms_per_step": round(fdt / a.steps * 1e3, 3),
+                "keypoints_per_s": round(fkp * a.steps / fdt, 1), "keypoints_per_step": int(fkp),
+                "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in fst.items()},
+                "note": "SIFT_FLAG_FAST: separable row/column Gaussian pyramid (pyramid_fast.hip) in front of "
+                        "the same exact DoG/extrema/orientation/descriptor kernels; not bit-exact (float "
+                        "rounding of the pyramid), keypoint/descriptor match rates vs the CPU path are in "
+                        "tests/test_gpu_fast.py"}
+            out["roofline_pyramid_fast"] = {
+                "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "pyr_fast_kernel",
+                "avg_launch_ms": round(pf["ms"] / max(pf["launches"], 1), 4),
+                "pyramid_ms_per_step": round(pf["ms"] / a.steps, 4),
+                "note": "algorithmic bytes B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes, "
+                        "SURVEY.md 8(d)) over the five per-octave launches of one step, / their summed "
+                        "HIP-event time; north_star target frac >= 0.6"}
         if world == 1 and not a.no_cpu_baseline:
             cb = cpu_baseline(R, C)
             out["cpu_baseline"] = cb

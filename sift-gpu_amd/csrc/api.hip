@@ -76,9 +76,9 @@ struct StageRec {
 
 const char* const kStageNames[] = {"blur_base", "blur_octave", "decimate", "dog", "extrema",
                                    "refine_orient", "emit", "descriptor", "upload", "download",
-                                   "blur_1d"};
+                                   "blur_1d", "pyramid_fast"};
 enum Stage { ST_BLUR_BASE, ST_BLUR_OCT, ST_DECIMATE, ST_DOG, ST_EXTREMA, ST_REFINE, ST_EMIT,
-             ST_DESC, ST_UPLOAD, ST_DOWNLOAD, ST_BLUR1D, ST_N };
+             ST_DESC, ST_UPLOAD, ST_DOWNLOAD, ST_BLUR1D, ST_PYR_FAST, ST_N };
 
 template <typename T>
 hipError_t dmalloc(T** p, size_t count) {
@@ -105,6 +105,7 @@ struct sift_ctx {
   long long gpyr_elems = 0, dog_elems = 0;
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
+  void* d_fast = nullptr;         // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip)
   size_t coef_gen_cap = 0;
   int wsz[4] = {0, 0, 0, 0};
   int w_base = 0;
@@ -238,6 +239,22 @@ double plane_px(const Layout& L, int o) { return (double)L.oct[o].rows * L.oct[o
 // input planes are described by src.  Async on c->stream.
 void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool with_dog) {
   hipStream_t st = c->stream;
+  if (c->flags & SIFT_FLAG_FAST) {
+    // separable pyramid: 24 algorithmic bytes per pixel (1 read + 5 plane
+    // writes); 2 x (row + column taps) flops per pixel
+    for (int o = 0; o < L.n_oct; ++o) {
+      const double px = plane_px(L, o) * batch;
+      const double taps = 2.0 * (9 + 17 + 25 + 37) + (o == 0 ? 2.0 * 9 : 0.0);
+      StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
+      launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->d_fast);
+    }
+    if (with_dog)
+      for (int o = 0; o < L.n_oct; ++o) {
+        StageScope s(c, ST_DOG, 4.0 * plane_px(L, o) * batch, 36.0 * plane_px(L, o) * batch);
+        launch_dog(st, L, o, c->d_gpyr, c->d_dog, batch);
+      }
+    return;
+  }
   {
     const double px = plane_px(L, 0) * batch;
     const int k = 2 * c->w_base + 1;
@@ -347,7 +364,7 @@ void verbose_phase(sift_ctx* c, const char* what, hipEvent_t a, hipEvent_t b) {
 
 extern "C" {
 
-const char* sift_version(void) { return "sift-hip 0.1 (gfx950, exact mode)"; }
+const char* sift_version(void) { return "sift-hip 0.2 (gfx950; exact + SIFT_FLAG_FAST separable pyramid)"; }
 
 int sift_octave_shapes(int rows, int cols, int n_octaves, int* orows, int* ocols) {
   if (n_octaves < 1 || n_octaves > kMaxOctaves || !orows || !ocols) return SIFT_E_INVALID;
@@ -404,8 +421,9 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   // Gaussian coefficients: base sigma sqrt(1.6^2 + 0.2^2) (src/sift.cpp:237)
   // and sig[1..4] (src/sift.cpp:240-245), each through getGaussianKernel(float).
   std::vector<float> coefs;
+  float sig_f[4] = {0, 0, 0, 0};
+  const float sb = (float)sqrt(kSigma * kSigma + 0.2 * 0.2);
   {
-    const float sb = (float)sqrt(kSigma * kSigma + 0.2 * 0.2);
     const int ks = gaussian_kernel_host(sb, nullptr);
     c->w_base = ks / 2;
     c->coef_base_off = 0;
@@ -416,6 +434,7 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     for (int i = 1; i < kScales; ++i) {
       const double tot = pow(k * 1.0, (double)i) * kSigma;
       const float sg = (float)sqrt(tot * tot - kSigma * kSigma);
+      sig_f[i - 1] = sg;
       const int kk = gaussian_kernel_host(sg, nullptr);
       c->wsz[i - 1] = kk / 2;
       const size_t at = coefs.size();
@@ -425,6 +444,11 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   }
   if (c->w_base != 4 || c->wsz[0] != 4 || c->wsz[1] != 8 || c->wsz[2] != 12 || c->wsz[3] != 18)
     return bail(SIFT_E_INVALID);  // the octave kernel is unrolled for these widths
+  std::vector<char> fast(fast_coefs_size());
+  if (fast_coefs_host(sb, sig_f, fast.data()) != 0) return bail(SIFT_E_INVALID);
+  if (hipMalloc(&c->d_fast, fast.size()) != hipSuccess) return bail(SIFT_E_NOMEM);
+  if (hipMemcpy(c->d_fast, fast.data(), fast.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return bail(SIFT_E_HIP);
   MathConsts mc;
   host_math_consts(&mc);
   if (dmalloc(&c->d_coef, coefs.size()) != hipSuccess || dmalloc(&c->d_mc, 1) != hipSuccess ||
@@ -468,7 +492,7 @@ int sift_ctx_destroy(sift_ctx* c) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : c->pool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
+  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_fast, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
                   c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->d_img_off,
                   c->d_kpts, c->d_desc, c->d_err};

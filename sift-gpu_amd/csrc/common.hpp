@@ -177,6 +177,15 @@ void launch_blur_1d(hipStream_t st, int w, const float* coef1d, Plane src, float
 void launch_synth(hipStream_t st, float* out, int batch, int rows, int cols, long long pitch,
                   long long img_stride, int seed_base);
 
+// pyramid_fast.hip (SIFT_FLAG_FAST): separable row/column pyramid, one launch
+// per octave writing its five planes.  Coefficient block built on the host:
+// fast_coefs_host(base sigma, sig[1..4], out[fast_coefs_size()]) != 0 if the
+// kernel widths are not the unrolled 4 / 4, 8, 12, 18.
+size_t fast_coefs_size();
+int fast_coefs_host(float sigma_base, const float* sig, void* out);
+void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
+                         const void* coef);
+
 // detect.hip
 struct DetectBufs {
   unsigned* mask;       // candidate bitmask, mask_words_per_image * batch

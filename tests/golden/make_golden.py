@@ -84,6 +84,11 @@ def case(name, img, with_planes=True, store_full=True):
 
 def main():
     O.build()
+    if "--8k" in sys.argv:
+        # configs[4]: one 7680x4320 image (digests only; about 2 minutes of CPU)
+        O.set_threads(os.cpu_count() or 1)
+        case("synth0_4320x7680", O.synth_image(0, 4320, 7680), store_full=False)
+        return
     if os.path.exists(BOOK):
         write_pgm(os.path.join(OUT, "book_gray.pgm"), book_gray())
     book = read_pgm(os.path.join(OUT, "book_gray.pgm")).astype(np.float32)
