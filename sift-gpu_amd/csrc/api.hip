@@ -105,7 +105,7 @@ struct sift_ctx {
   long long gpyr_elems = 0, dog_elems = 0;
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
-  void* d_fast = nullptr;         // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip)
+  std::vector<char> fast_taps;    // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip), passed by value
   size_t coef_gen_cap = 0;
   int wsz[4] = {0, 0, 0, 0};
   int w_base = 0;
@@ -246,7 +246,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       const double px = plane_px(L, o) * batch;
       const double taps = 2.0 * (9 + 17 + 25 + 37) + (o == 0 ? 2.0 * 9 : 0.0);
       StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-      launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->d_fast);
+      launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
     }
     if (with_dog)
       for (int o = 0; o < L.n_oct; ++o) {
@@ -444,11 +444,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   }
   if (c->w_base != 4 || c->wsz[0] != 4 || c->wsz[1] != 8 || c->wsz[2] != 12 || c->wsz[3] != 18)
     return bail(SIFT_E_INVALID);  // the octave kernel is unrolled for these widths
-  std::vector<char> fast(fast_coefs_size());
-  if (fast_coefs_host(sb, sig_f, fast.data()) != 0) return bail(SIFT_E_INVALID);
-  if (hipMalloc(&c->d_fast, fast.size()) != hipSuccess) return bail(SIFT_E_NOMEM);
-  if (hipMemcpy(c->d_fast, fast.data(), fast.size(), hipMemcpyHostToDevice) != hipSuccess)
-    return bail(SIFT_E_HIP);
+  c->fast_taps.resize(fast_coefs_size());
+  if (fast_coefs_host(sb, sig_f, c->fast_taps.data()) != 0) return bail(SIFT_E_INVALID);
   MathConsts mc;
   host_math_consts(&mc);
   if (dmalloc(&c->d_coef, coefs.size()) != hipSuccess || dmalloc(&c->d_mc, 1) != hipSuccess ||
@@ -492,7 +489,7 @@ int sift_ctx_destroy(sift_ctx* c) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : c->pool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_fast, c->d_mc,
+  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
                   c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->d_img_off,
                   c->d_kpts, c->d_desc, c->d_err};

@@ -27,9 +27,10 @@ def main():
     p.add_argument("--cols", type=int, default=1920)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--tag", default="")
+    p.add_argument("--fast", action="store_true", help="SIFT_FLAG_FAST pyramid")
     a = p.parse_args()
     B, R, C = a.batch, a.rows, a.cols
-    ctx = siftgpu.Context(R, C, B, flags=siftgpu.SIFT_FLAG_PROFILE)
+    ctx = siftgpu.Context(R, C, B, flags=siftgpu.SIFT_FLAG_PROFILE | (siftgpu.SIFT_FLAG_FAST if a.fast else 0))
     imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
     ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, 0)
     cap = B * 40000
