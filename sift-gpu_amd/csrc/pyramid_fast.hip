@@ -19,18 +19,25 @@
 // so every row pass is done once per row (the vertical halo is carried in the
 // rings, not recomputed) and every source pixel is read from HBM once (plus
 // an 18-column halo that hits L2).  Bound: HBM, 24 algorithmic bytes per pixel
-// (one read, five plane writes) against ~180 FMA per pixel.
+// (one read, five plane writes) against ~194 FMA per pixel.
 //
-// Latency structure (what the profile showed mattered):
-//  * the next step's source rows are loaded into registers while the current
-//    step computes, and every load is branch-free (clamped address + select);
+// What the profile showed mattered:
+//  * FMA issue.  Every FMA stream is written on pairs (v_pk_fma_f32: twice
+//    the rate of v_fma_f32 from one or two waves per SIMD, measured by
+//    tools/ubench_fma.hip), with both operands of every pair in aligned
+//    registers straight from LDS: row passes pair two rows (the base / image
+//    rows are staged row-pair interleaved, so one ds_read_b128 yields two
+//    columns of two rows), column passes pair two columns (ds_read_b64);
+//  * the taps come from the kernel-argument segment with scalar loads issued
+//    per pass (fresh()), not held in SGPRs across the loop (spills);
+//  * the next step's source rows are loaded during the column passes with
+//    loads hipcc does not track and waited for with an explicit vmcnt (see
+//    ld2_async); every load is branch-free (clamped address, the padding
+//    select happens when the values are staged);
 //  * plane stores go through a buffer resource: an invalid position gets an
-//    out-of-range offset and the hardware drops the store, so each step issues
-//    a fixed number of stores.  hipcc can then wait for the prefetch with
-//    vmcnt(N) instead of vmcnt(0), and the stores stay in flight across the
-//    step boundary (with data-dependent store counts every step waited for
-//    all of its stores to reach memory: 40% of the kernel time);
-//  * the taps are kernel arguments (scalar cache), not VMEM loads;
+//    out-of-range offset and the hardware drops the store, so each wave
+//    issues a fixed number of stores per step and the wait for the prefetch
+//    can leave them in flight;
 //  * steps start on a multiple of 8 and every ring holds a multiple of 8
 //    rows, so a column pass starts at one of M/8 ring slots and each start is
 //    its own unrolled body with compile-time LDS offsets.
@@ -48,12 +55,14 @@ constexpr int kRB = 8;                 // rows per step
 constexpr int kH = 18;                 // widest scale half-width (sig[4] = 6.197)
 constexpr int kLead = 24;              // base rows computed above the chunk (>= kH, multiple of 8)
 constexpr int kBW = kFW + 2 * kH;      // 164 base columns per strip
-constexpr int kBP = 172;               // base / row-pass ring pitch (== 4 mod 8)
-constexpr int kIP = 180;               // image staging pitch (176 columns used)
-constexpr int kIQ = 44;                // float4 per staged image row
+constexpr int kIW = 176;               // staged image columns [x0-24, x0+152)
+constexpr int kSP = 356;               // staged image row-pair pitch (floats; 2 x 176 + 4)
+constexpr int kBP2 = 332;              // base row-pair pitch (floats; 2 x 164 + 4, == 4 mod 8)
+constexpr int kBP = 172;               // octave-0 row-pass ring pitch (168 columns used)
 constexpr int kRP = 132;               // scale ring pitch (== 4 mod 8)
 constexpr int kHbRows = 16;            // octave-0 row-pass ring: rows [Z-4, Z+12)
-constexpr int kStage = kRB * kIP;      // staged image rows / base rows (aliased)
+constexpr int kStage = 4 * kSP;        // staged image row pairs / base row pairs (aliased)
+constexpr int kImgUnits = 4 * (kIW / 2);          // 2 rows x 2 columns per unit: 352 per step
 constexpr int kGather = (kRB * kBW + 255) / 256;  // decimation gathers per lane per step
 constexpr int kDrop = 0x7ffffff0;      // buffer offset past every plane: the store is dropped
 
@@ -67,13 +76,17 @@ constexpr int kRingRows = 120;
 
 constexpr int kLds0 = kStage + kHbRows * kBP + kRingRows * kRP;   // floats, octave 0
 constexpr int kLdsN = kStage + kRingRows * kRP + kBW;             // floats (+ column map), octave > 0
-static_assert(kRB * kBP <= kStage, "base rows alias the image staging rows");
-static_assert(kBP % 8 == 4 && kRP % 8 == 4 && kIP % 4 == 0, "b128 row pitches");
+static_assert(4 * kBP2 <= kStage, "base row pairs alias the image staging rows");
+static_assert(kSP % 4 == 0 && kBP2 % 8 == 4 && kBP % 4 == 0 && kRP % 8 == 4, "b128 row pitches");
 static_assert(kLds0 % 4 == 0 && kLdsN % 4 == 0 && kStage % 4 == 0 && (kHbRows * kBP) % 4 == 0,
               "float4 LDS regions");
 static_assert(2 * kLds0 * 4 <= 160 * 1024, "two workgroups per CU");
+static_assert(kGather == 6, "SIFT_VM_WAIT operand list");
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
+typedef const __attribute__((address_space(4))) float* Taps;  // see fresh()
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ Rsrc plane_rsrc(float* p, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)bytes, 0x00020000);
@@ -83,98 +96,124 @@ __device__ __forceinline__ void st_plane(Rsrc rs, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, off, 0, 0);
 }
 
-// LDS pointers are float4 arrays indexed in float4 units, so every address is
-// provably 16-byte aligned and hipcc emits ds_read_b128 / ds_write_b128.
-//
-// Row pass of one scale: h[Z + r][8j + p] = sum_b g[b] base[r][8j + p + 18 - W + b].
-// The 16-lane groups of a ds_read_b128 hold two whole base rows x 8 column
-// groups; with kBP == 4 (mod 8) their 16-byte slots are distinct (conflict free).
-template <int W>
-__device__ __forceinline__ void row_pass(const float4* __restrict__ bs4, float4* __restrict__ rings4,
-                                         const float* __restrict__ g, int r, int j, int slot) {
-  constexpr int ST = (kH - W) & ~3, E = (kH - W) & 3;
-  constexpr int L = (E + kRB + 2 * W + 3) & ~3;
-  float win[L];
-  const float4* src = bs4 + r * (kBP / 4) + 2 * j + ST / 4;
+__device__ __forceinline__ void st_plane2(Rsrc rs, int off, f2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rs, off, 0, 0);
+}
+
+// Window reads of the column passes.  hipcc pairs two ds_read_b64 off one
+// base register that are < 2 KB apart into a ds_read2_b64, which moves half as
+// many bytes per LDS cycle (8 cycles for 2 x 8 B per lane against 2 x 2).  The
+// window rows are read off four opaque copies of the base, row k off copy
+// k & 3: rows on one copy are >= 4 ring rows (> 2 KB) apart, so no pair forms.
+typedef const __attribute__((address_space(3))) f2* LdsF2;
+
+template <int NB>
+__device__ __forceinline__ void lds_bases(const f2* p, LdsF2 (&b)[NB]) {
 #pragma unroll
-  for (int q = 0; q < L / 4; ++q) {
-    const float4 t = src[q];
-    win[4 * q] = t.x;
-    win[4 * q + 1] = t.y;
-    win[4 * q + 2] = t.z;
-    win[4 * q + 3] = t.w;
+  for (int i = 0; i < NB; ++i) {
+    b[i] = (LdsF2)p;
+    asm volatile("" : "+v"(b[i]));
   }
-  // Keep the whole 16-byte loads: hipcc trims unused leading / trailing floats
-  // and then falls back to 8-byte-aligned ds_read2_b64 (4-way bank conflicts).
+}
+
+// Two independent fmaf in one v_pk_fma_f32; each element is still the same
+// sequential fmaf chain as the scalar form.
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+__device__ __forceinline__ f2 splat(float k) { return f2{k, k}; }
+
+// Row pass of one scale for base rows (2s, 2s+1) and output columns
+// [4j, 4j+4): h[Z + 2s + e][4j + i] = sum_b g[b] base[2s + e][4j + i + 18 - W + b].
+// The base rows are staged row-pair interleaved (bs2[s][c] = (row 2s, row
+// 2s+1) at column c), so each pk_fma operand is an aligned register pair of a
+// ds_read_b128.  Lane -> (s, j) puts two row pairs x 8 column groups in each
+// 16-lane group of a ds_read_b128; with kBP2 == 4 (mod 8) their 16-byte slots
+// are distinct (conflict free).  The two output rows are written with
+// ds_write_b128 (8 contiguous lanes per group: conflict free).
+template <int W>
+__device__ __forceinline__ void row_pass(const float4* __restrict__ bs4, float4* __restrict__ rings4, Taps g,
+                                         int s, int j, int slot) {
+  constexpr int C0 = kH - W, NW = 4 + 2 * W;
+  static_assert(C0 % 2 == 0 && NW % 2 == 0, "windows start on a column pair");
+  const float4* src = bs4 + s * (kBP2 / 4) + 2 * j + C0 / 2;
+  f2 w[NW];
 #pragma unroll
-  for (int k = 0; k < L; ++k)
-    if (k < E || k >= E + kRB + 2 * W) asm volatile("" ::"v"(win[k]));
-  float acc[8];
+  for (int q = 0; q < NW / 2; ++q) {
+    const float4 v = src[q];
+    w[2 * q] = f2{v.x, v.y};
+    w[2 * q + 1] = f2{v.z, v.w};
+  }
+  f2 acc[4];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) acc[p] = 0.f;
+  for (int i = 0; i < 4; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int b = 0; b <= 2 * W; ++b) {
-    const float k = g[b];
+    const f2 k = splat(g[b]);
 #pragma unroll
-    for (int p = 0; p < 8; ++p) acc[p] = __builtin_fmaf(win[E + p + b], k, acc[p]);
+    for (int i = 0; i < 4; ++i) acc[i] = pk_fma(w[i + b], k, acc[i]);
   }
-  // ds_write_b128 serves 8 lanes (8 x 16 B = 32 banks) per cycle: lanes j and
-  // j + 4 would collide at stride 32 B, so the upper half-group writes its two
-  // halves in the other order.
-  float4* dst = rings4 + (Ring<W>::off + slot) * (kRP / 4) + 2 * j;
-  const float4 lo = make_float4(acc[0], acc[1], acc[2], acc[3]);
-  const float4 hi = make_float4(acc[4], acc[5], acc[6], acc[7]);
-  if (j & 4) {
-    dst[1] = hi;
-    dst[0] = lo;
-  } else {
-    dst[0] = lo;
-    dst[1] = hi;
-  }
+  // slot + 1 never wraps: slot = (Z - rbase) mod M + 2s with Z - rbase and M
+  // multiples of 8.
+  float4* dst = rings4 + (Ring<W>::off + slot) * (kRP / 4) + j;
+  dst[0] = make_float4(acc[0].x, acc[1].x, acc[2].x, acc[3].x);
+  dst[kRP / 4] = make_float4(acc[0].y, acc[1].y, acc[2].y, acc[3].y);
 }
 
-// Column pass of one scale starting at ring slot S0: rows [Z - W, Z - W + 8)
-// of the plane, column x, from ring rows [Z - 2W, Z + 8).  Always stores 8
-// values; rows outside [y0, y1) and columns past the image are dropped.
-template <int W, int S0>
-__device__ __forceinline__ void col_fixed(const float* __restrict__ rings, const float* __restrict__ g,
-                                          int col, Rsrc rs, int pitch, int x, int Z, int y0, int y1,
-                                          bool colok) {
-  constexpr int M = Ring<W>::M, N = kRB + 2 * W;
-  const float* ring = rings + Ring<W>::off * kRP + col;
-  float win[N];
+// Column pass of one scale, two columns per lane: plane rows [Y, Y + NR),
+// columns x, x+1, from ring rows [Y - W, Y + NR + W) starting at ring slot S0
+// (ds_read_b64: 32 contiguous lanes per group, conflict free).  Always issues
+// NR (8-byte) stores; rows outside [y0, y1) and column pairs past the image
+// are dropped (a pair that straddles an odd image width also writes the pitch
+// padding column, which nothing reads).
+template <int W, int S0, int NR>
+__device__ __forceinline__ void col_fixed(const float* __restrict__ rings, Taps g, int lane, Rsrc rs, int pitch,
+                                          int x, int Y, int y0, int y1, bool colok) {
+  constexpr int M = Ring<W>::M, N = NR + 2 * W;
+  LdsF2 ring[4];
+  lds_bases(reinterpret_cast<const f2*>(rings + Ring<W>::off * kRP) + lane, ring);
+  f2 win[N];
 #pragma unroll
-  for (int k = 0; k < N; ++k) win[k] = ring[((S0 + k) % M) * kRP];
-  float acc[8];
+  for (int k = 0; k < N; ++k) win[k] = ring[k & 3][((S0 + k) % M) * (kRP / 2)];
+  f2 acc[NR];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int i = 0; i < NR; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int a = 0; a <= 2 * W; ++a) {
-    const float k = g[a];
+    const f2 k = splat(g[a]);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = __builtin_fmaf(win[i + a], k, acc[i]);
+    for (int i = 0; i < NR; ++i) acc[i] = pk_fma(win[i + a], k, acc[i]);
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int y = Z - W + i;
-    st_plane(rs, (colok && y >= y0 && y < y1) ? (y * pitch + x) * 4 : kDrop, acc[i]);
+  for (int i = 0; i < NR; ++i) {
+    const int y = Y + i;
+    st_plane2(rs, (colok && y >= y0 && y < y1) ? (y * pitch + x) * 4 : kDrop, acc[i]);
+  }
+  // A distinct tail per body: otherwise hipcc sinks the (identical) FMA and
+  // store code of the M/8 bodies into one and moves every window into it with
+  // v_mov -- N extra VALU per pass, and the compile-time offsets lost.
+  asm volatile("; col_fixed %0 %1 %2" ::"n"(W), "n"(S0), "n"(NR));
+}
+
+// Rows [Z - W + R, +NR) of the plane.  Their window starts at ring slot
+// s0 = (Z - 2W + R - rbase) mod M = 8c + R0 with R0 = (R - 2W) mod 8 (steps
+// and rbase are multiples of 8): uniform dispatch to the body for c.
+template <int W, int NR, int R, int C>
+__device__ __forceinline__ void col_pass(int c, const float* __restrict__ rings, Taps g, int lane, Rsrc rs,
+                                         int pitch, int x, int Z, int y0, int y1, bool colok) {
+  constexpr int R0 = (((R - 2 * W) % 8) + 8) % 8;
+  if constexpr (C + 1 < Ring<W>::M / 8) {
+    if (c == C)
+      col_fixed<W, 8 * C + R0, NR>(rings, g, lane, rs, pitch, x, Z - W + R, y0, y1, colok);
+    else
+      col_pass<W, NR, R, C + 1>(c, rings, g, lane, rs, pitch, x, Z, y0, y1, colok);
+  } else {
+    col_fixed<W, 8 * C + R0, NR>(rings, g, lane, rs, pitch, x, Z - W + R, y0, y1, colok);
   }
 }
 
-// Start slot s0 = 8c + R0 (R0 = -2W mod 8): uniform dispatch to the body for c.
-template <int W, int C>
-__device__ __forceinline__ void col_pass(int c, const float* __restrict__ rings, const float* __restrict__ g,
-                                         int col, Rsrc rs, int pitch, int x, int Z, int y0, int y1,
-                                         bool colok) {
-  constexpr int R0 = (8 - (2 * W) % 8) % 8;
-  if constexpr (C + 1 < Ring<W>::M / 8) {
-    if (c == C)
-      col_fixed<W, 8 * C + R0>(rings, g, col, rs, pitch, x, Z, y0, y1, colok);
-    else
-      col_pass<W, C + 1>(c, rings, g, col, rs, pitch, x, Z, y0, y1, colok);
-  } else {
-    col_fixed<W, 8 * C + R0>(rings, g, col, rs, pitch, x, Z, y0, y1, colok);
-  }
+template <int W, int R>
+__device__ __forceinline__ int col_slot(int Z, int rbase) {
+  return ((Z - 2 * W + R - rbase) % Ring<W>::M) >> 3;
 }
 
 }  // namespace
@@ -194,67 +233,122 @@ struct FastArgs {
   int pitch, rows, cols;
   int srows, scols;        // source (previous octave) shape
   int chunk;               // rows per workgroup (multiple of kRB)
-  int ablate;              // diagnostic only (SIFT_FAST_ABLATE): 4 skips the row passes
-  // By value: kernel arguments are constant memory, so the taps come through
-  // the scalar cache.  Through a pointer the compiler cannot rule out that the
-  // plane stores alias them and reloads every tap with a VMEM load per pass.
-  FastCoefs coef;
+  FastCoefs coef;          // by value: read in the kernel through fresh()
 };
 
 namespace {
 
-// Octave-0 image rows [Y, Y+8) x columns [x0-24, x0+152) -> 2 float4 per lane
-// (lanes >= 96 hold one), loaded from clamped addresses with no branch and no
-// use: the padding select happens in put_image, a step later, so the loads
-// stay in flight.  VEC: rows are 16-byte aligned with a pitch that is a
-// multiple of 4 (>= cols), so a float4 at a clamped x never leaves the row.
+// The taps are read from the kernel-argument segment (scalar loads that no
+// plane store can alias) through a pointer made opaque at each pass, so hipcc
+// loads each pass's taps right before the pass instead of keeping all 97 live
+// across the step loop (which spilled ~290 SGPRs to VGPR lanes and cost a
+// v_readlane per tap use).
+typedef const __attribute__((address_space(4))) FastArgs* KArgs;
+
+__device__ __forceinline__ KArgs fresh(KArgs p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// Source prefetch with loads the compiler does not track (inline asm).  With
+// ordinary loads hipcc counted VMEM operations conservatively across the
+// column passes' branches and waited for most of a step's plane stores to
+// reach memory before it let a prefetched value be used.  Here the loads are
+// issued right before the column passes and waited for right after them with
+// vmcnt(n) -- n = the stores this wave's column passes issue (fixed per wave)
+// and VMEM operations retire in order -- so the stores stay in flight into the
+// next step.  The destination registers are operands of the wait, so nothing
+// reads them before it.
+__device__ __forceinline__ f2 ld2_async(const float* p) {
+  f2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+
+__device__ __forceinline__ float ld1_async(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+
+struct Pre {         // one step's prefetched source values
+  f2 v[4];           // octave 0, 8-byte rows: units (t, t+256) x rows (2s, 2s+1)
+  float s[8];        // octave 0, unaligned rows: the same, element by element
+  float g[kGather];  // octave > 0
+};
+
+#define SIFT_VM_WAIT(CNT)                                                                                  \
+  do {                                                                                                     \
+    if constexpr (OCT0 && VEC) {                                                                           \
+      asm volatile("s_waitcnt vmcnt(" #CNT ")"                                                             \
+                   : "+v"(P.v[0]), "+v"(P.v[1]), "+v"(P.v[2]), "+v"(P.v[3])::"memory");                    \
+    } else if constexpr (OCT0) {                                                                           \
+      asm volatile("s_waitcnt vmcnt(" #CNT ")"                                                             \
+                   : "+v"(P.s[0]), "+v"(P.s[1]), "+v"(P.s[2]), "+v"(P.s[3]), "+v"(P.s[4]), "+v"(P.s[5]),   \
+                     "+v"(P.s[6]), "+v"(P.s[7])::"memory");                                                \
+    } else {                                                                                               \
+      asm volatile("s_waitcnt vmcnt(" #CNT ")"                                                             \
+                   : "+v"(P.g[0]), "+v"(P.g[1]), "+v"(P.g[2]), "+v"(P.g[3]), "+v"(P.g[4]),                 \
+                     "+v"(P.g[5])::"memory");                                                              \
+    }                                                                                                      \
+  } while (0)
+
+// Octave-0 image rows [Y, Y+8) x columns [x0-24, x0+152) in units of 2 rows x
+// 2 columns (unit i: row pair s = i / 88, column pair q = i % 88); lanes hold
+// units t and t + 256 (< 352), from clamped addresses.  VEC: rows are 16-byte
+// aligned with a pitch that is a multiple of 4 (>= cols), so a float2 at a
+// clamped even x never leaves the row.
 template <bool VEC>
-__device__ __forceinline__ void fetch_image(const FastArgs& A, const float* __restrict__ img, int x0,
-                                            int Y, float4 (&v)[2]) {
+__device__ __forceinline__ void fetch_image(const FastArgs& A, const float* __restrict__ img, int x0, int Y,
+                                            Pre& P) {
   const int lim = A.cols - 1;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int i = threadIdx.x + 256 * u;
-    const int r = i / kIQ, q = i - r * kIQ;
-    const int y = Y + r, x = x0 - 24 + 4 * q;
-    const float* row = img + (long long)min(max(y, 0), A.rows - 1) * A.s_pitch;
+    const int s = i / (kIW / 2), q = i - s * (kIW / 2);
+    const int y = Y + 2 * s, x = x0 - 24 + 2 * q;
+    const float* r0 = img + (long long)min(max(y, 0), A.rows - 1) * A.s_pitch;
+    const float* r1 = img + (long long)min(max(y + 1, 0), A.rows - 1) * A.s_pitch;
     if (VEC) {
-      v[u] = *reinterpret_cast<const float4*>(row + min(max(x, 0), (int)A.s_pitch - 4));
+      const int xv = min(max(x, 0), (int)A.s_pitch - 2);
+      P.v[2 * u] = ld2_async(r0 + xv);
+      P.v[2 * u + 1] = ld2_async(r1 + xv);
     } else {
-      v[u].x = row[min(max(x, 0), lim)];
-      v[u].y = row[min(max(x + 1, 0), lim)];
-      v[u].z = row[min(max(x + 2, 0), lim)];
-      v[u].w = row[min(max(x + 3, 0), lim)];
+      const int xa = min(max(x, 0), lim), xb = min(max(x + 1, 0), lim);
+      P.s[4 * u] = ld1_async(r0 + xa);
+      P.s[4 * u + 1] = ld1_async(r0 + xb);
+      P.s[4 * u + 2] = ld1_async(r1 + xa);
+      P.s[4 * u + 3] = ld1_async(r1 + xb);
     }
   }
 }
 
-// Writes the fetched rows [Y, Y+8) to the staging rows with the source padding
-// of the base blur: 0 outside [0, rows-1) x [0, cols-1).
-__device__ __forceinline__ void put_image(const FastArgs& A, float4* __restrict__ stage4, const float4 (&v)[2],
-                                          int x0, int Y) {
+// Stages the fetched units row-pair interleaved, (r0 c, r1 c, r0 c+1, r1 c+1),
+// with the source padding of the base blur: 0 outside [0, rows-1) x [0, cols-1).
+template <bool VEC>
+__device__ __forceinline__ void put_image(const FastArgs& A, float4* __restrict__ stage4, const Pre& P, int x0,
+                                          int Y) {
   const int lim = A.cols - 1;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int i = threadIdx.x + 256 * u;
-    if (i < kRB * kIQ) {
-      const int r = i / kIQ, q = i - r * kIQ;
-      const int y = Y + r, x = x0 - 24 + 4 * q;
-      const bool rowok = y >= 0 && y < A.rows - 1;
-      float4 w;
-      w.x = (rowok && x >= 0 && x < lim) ? v[u].x : 0.f;
-      w.y = (rowok && x + 1 >= 0 && x + 1 < lim) ? v[u].y : 0.f;
-      w.z = (rowok && x + 2 >= 0 && x + 2 < lim) ? v[u].z : 0.f;
-      w.w = (rowok && x + 3 >= 0 && x + 3 < lim) ? v[u].w : 0.f;
-      stage4[r * (kIP / 4) + q] = w;
+    if (i < kImgUnits) {
+      const int s = i / (kIW / 2), q = i - s * (kIW / 2);
+      const int y = Y + 2 * s, x = x0 - 24 + 2 * q;
+      const bool ok0 = y >= 0 && y < A.rows - 1, ok1 = y + 1 >= 0 && y + 1 < A.rows - 1;
+      const bool oka = x >= 0 && x < lim, okb = x + 1 >= 0 && x + 1 < lim;
+      const float a0 = VEC ? P.v[2 * u].x : P.s[4 * u], b0 = VEC ? P.v[2 * u].y : P.s[4 * u + 1];
+      const float a1 = VEC ? P.v[2 * u + 1].x : P.s[4 * u + 2], b1 = VEC ? P.v[2 * u + 1].y : P.s[4 * u + 3];
+      stage4[s * (kSP / 4) + q] = make_float4((ok0 && oka) ? a0 : 0.f, (ok1 && oka) ? a1 : 0.f,
+                                              (ok0 && okb) ? b0 : 0.f, (ok1 && okb) ? b1 : 0.f);
     }
   }
 }
 
 // Octave > 0: the INTER_NEAREST source values of base rows [Z, Z+8) (source
-// row min(floor(y * ify), srows-1), column map in LDS), branch-free loads.
+// row min(floor(y * ify), srows-1), column map in LDS), clamped addresses.
 __device__ __forceinline__ void fetch_decim(const FastArgs& A, const float* __restrict__ prev,
-                                            const int* __restrict__ xmap, int Z, float (&v)[kGather]) {
+                                            const int* __restrict__ xmap, int Z, Pre& P) {
 #pragma unroll
   for (int u = 0; u < kGather; ++u) {
     const int i = threadIdx.x + 256 * u;
@@ -264,84 +358,112 @@ __device__ __forceinline__ void fetch_decim(const FastArgs& A, const float* __re
     const bool ok = i < kRB * kBW && y >= 0 && y < A.rows && sx >= 0;
     int sy = (int)floor(max(y, 0) * A.ify);
     sy = sy < A.srows - 1 ? sy : A.srows - 1;
-    v[u] = prev[ok ? (long long)sy * A.s_pitch + sx : 0];
+    P.g[u] = ld1_async(prev + (ok ? (long long)sy * A.s_pitch + sx : 0));
+  }
+}
+
+// Octave > 0: base rows [Z, Z+8) from the prefetched decimation values: the
+// plane-0 interior (unpadded) to HBM and the padded copy (0 outside
+// [0, rows-1) x [0, cols-1)) into the row-pair interleaved base rows.
+__device__ __forceinline__ void put_decim(const FastArgs& A, float* __restrict__ bs, Rsrc rs0,
+                                          const int* __restrict__ xmap, const Pre& P, int Z, int x0, int y0,
+                                          int y1) {
+#pragma unroll
+  for (int u = 0; u < kGather; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i < kRB * kBW) {
+      const int r = i / kBW, c = i - r * kBW;
+      const int y = Z + r, x = x0 - kH + c;
+      const float v = (y >= 0 && y < A.rows && xmap[c] >= 0) ? P.g[u] : 0.f;
+      const bool out = c >= kH && c < kH + kFW && x < A.cols && y >= y0 && y < y1;
+      st_plane(rs0, out ? (y * A.pitch + x) * 4 : kDrop, v);
+      const bool src_ok = y >= 0 && y < A.rows - 1 && x >= 0 && x < A.cols - 1;
+      bs[(r >> 1) * kBP2 + 2 * c + (r & 1)] = src_ok ? v : 0.f;
+    }
   }
 }
 
 // Octave-0 row pass of the base blur: ring rows [Y, Y+8), base columns
-// [0, 168) (column c <-> image column x0 - 18 + c; 164 are used).
-__device__ __forceinline__ void hb_pass(const float4* __restrict__ stage4, float4* __restrict__ hb4,
-                                        const float* __restrict__ g, int Y) {
+// [0, 164) (column c <-> image column x0 - 18 + c); lane t < 164 does row pair
+// s = t / 41, columns [4j, 4j+4), j = t % 41, from staged columns
+// [4j+2, 4j+14).
+__device__ __forceinline__ void hb_pass(const float4* __restrict__ stage4, float4* __restrict__ hb4, Taps g,
+                                        int Y) {
   const int t = threadIdx.x;
-  if (t >= kRB * 21) return;
-  const int r = t / 21, j = t - r * 21;
-  float win[20];
-  const float4* src = stage4 + r * (kIP / 4) + 2 * j;
+  if (t >= 4 * 41) return;
+  const int s = t / 41, j = t - s * 41;
+  const float4* src = stage4 + s * (kSP / 4) + 2 * j + 1;
+  f2 w[12];
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
+  for (int q = 0; q < 6; ++q) {
     const float4 v = src[q];
-    win[4 * q] = v.x;
-    win[4 * q + 1] = v.y;
-    win[4 * q + 2] = v.z;
-    win[4 * q + 3] = v.w;
+    w[2 * q] = f2{v.x, v.y};
+    w[2 * q + 1] = f2{v.z, v.w};
   }
-  asm volatile("" ::"v"(win[0]), "v"(win[1]), "v"(win[18]), "v"(win[19]));  // see row_pass
-  float acc[8];
+  f2 acc[4];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) acc[p] = 0.f;
+  for (int i = 0; i < 4; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int b = 0; b < 9; ++b) {
-    const float k = g[b];
+    const f2 k = splat(g[b]);
 #pragma unroll
-    for (int p = 0; p < 8; ++p) acc[p] = __builtin_fmaf(win[p + b + 2], k, acc[p]);
+    for (int i = 0; i < 4; ++i) acc[i] = pk_fma(w[i + b], k, acc[i]);
   }
-  float4* dst = hb4 + ((Y + r) & (kHbRows - 1)) * (kBP / 4) + 2 * j;
-  dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-  dst[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  hb4[((Y + 2 * s) & (kHbRows - 1)) * (kBP / 4) + j] = make_float4(acc[0].x, acc[1].x, acc[2].x, acc[3].x);
+  hb4[((Y + 2 * s + 1) & (kHbRows - 1)) * (kBP / 4) + j] = make_float4(acc[0].y, acc[1].y, acc[2].y, acc[3].y);
 }
 
-// Stores one base value: the plane-0 interior (unpadded) to HBM and the
-// padded copy (0 outside [0, rows-1) x [0, cols-1)) as the scales' source.
-__device__ __forceinline__ void put_base(const FastArgs& A, float* __restrict__ bs, Rsrc rs0, int r, int c,
-                                         int y, int x, int y0, int y1, float v) {
-  const bool out = c >= kH && c < kH + kFW && x < A.cols && y >= y0 && y < y1;
-  st_plane(rs0, out ? (y * A.pitch + x) * 4 : kDrop, v);
-  const bool src_ok = y >= 0 && y < A.rows - 1 && x >= 0 && x < A.cols - 1;
-  bs[r * kBP + c] = src_ok ? v : 0.f;
-}
-
-// Octave-0 column pass of the base blur for base rows [Z, Z+8), from row-pass
-// ring rows [Z-4, Z+12) starting at slot S0 = (Z - 4) & 15.
+// Octave-0 column pass of the base blur for base rows [Z, Z+8) and base
+// columns (2p, 2p+1), from row-pass ring rows [Z-4, Z+12) starting at slot
+// S0 = (Z - 4) & 15.  Writes the plane-0 interior to HBM and the padded copy
+// (0 outside [0, rows-1) x [0, cols-1)) into the row-pair interleaved base
+// rows.  c = 2p is even, so a pair is entirely inside or outside the strip's
+// output columns.
 template <int S0>
-__device__ __forceinline__ void base_col(const FastArgs& A, const float* __restrict__ hb, float* __restrict__ bs,
-                                         Rsrc rs0, int t, int Z, int x0, int y0, int y1) {
-  float win[16];
+__device__ __forceinline__ void base_col(const FastArgs& A, Taps g, const float* __restrict__ hb,
+                                         float4* __restrict__ bs4, Rsrc rs0, int p, int Z, int x0, int y0,
+                                         int y1) {
+  LdsF2 h2[4];  // see lds_bases (hb rows are 688 B apart)
+  lds_bases(reinterpret_cast<const f2*>(hb) + p, h2);
+  f2 win[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) win[k] = hb[((S0 + k) & (kHbRows - 1)) * kBP + t];
-  float acc[8];
+  for (int k = 0; k < 16; ++k) win[k] = h2[k & 3][((S0 + k) & (kHbRows - 1)) * (kBP / 2)];
+  f2 acc[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int i = 0; i < 8; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int a = 0; a < 9; ++a) {
-    const float k = A.coef.base[a];
+    const f2 k = splat(g[a]);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = __builtin_fmaf(win[i + a], k, acc[i]);
+    for (int i = 0; i < 8; ++i) acc[i] = pk_fma(win[i + a], k, acc[i]);
   }
+  const int c = 2 * p, x = x0 - kH + c;
+  const bool colout = c >= kH && c < kH + kFW && x < A.cols;
+  const bool oka = x >= 0 && x < A.cols - 1, okb = x + 1 >= 0 && x + 1 < A.cols - 1;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) put_base(A, bs, rs0, i, t, Z + i, x0 - kH + t, y0, y1, acc[i]);
+  for (int s = 0; s < 4; ++s) {
+    const int y = Z + 2 * s;
+    const f2 e0 = acc[2 * s], e1 = acc[2 * s + 1];
+    st_plane2(rs0, (colout && y >= y0 && y < y1) ? (y * A.pitch + x) * 4 : kDrop, e0);
+    st_plane2(rs0, (colout && y + 1 >= y0 && y + 1 < y1) ? ((y + 1) * A.pitch + x) * 4 : kDrop, e1);
+    const bool ok0 = y >= 0 && y < A.rows - 1, ok1 = y + 1 >= 0 && y + 1 < A.rows - 1;
+    bs4[s * (kBP2 / 4) + p] = make_float4((ok0 && oka) ? e0.x : 0.f, (ok1 && oka) ? e1.x : 0.f,
+                                          (ok0 && okb) ? e0.y : 0.f, (ok1 && okb) ? e1.y : 0.f);
+  }
+  asm volatile("; base_col %0" ::"n"(S0));  // see col_fixed
 }
 
 template <bool OCT0, bool VEC>
 __global__ __launch_bounds__(256, 2) void pyr_fast_kernel(FastArgs A) {
   __shared__ float4 lds4[(OCT0 ? kLds0 : kLdsN) / 4];
   float* const lds = reinterpret_cast<float*>(lds4);
+  float4* const stage4 = lds4;  // staged image row pairs (octave 0) / base row pairs
   float* const stage = lds;
-  float4* const stage4 = lds4;
-  float* const hb = lds + kStage;  // octave 0 only
-  float4* const hb4 = lds4 + kStage / 4;
+  float4* const hb4 = lds4 + kStage / 4;  // octave 0 only
+  const float* const hb = lds + kStage;
   float4* const rings4 = lds4 + (kStage + (OCT0 ? kHbRows * kBP : 0)) / 4;
-  float* const rings = reinterpret_cast<float*>(rings4);
-  int* const xmap = reinterpret_cast<int*>(rings + kRingRows * kRP);  // octave > 0 only
+  const float* const rings = reinterpret_cast<const float*>(rings4);
+  int* const xmap = reinterpret_cast<int*>(lds + kStage + kRingRows * kRP);  // octave > 0 only
 
   const int t = threadIdx.x;
   const int b = blockIdx.z;
@@ -352,21 +474,24 @@ __global__ __launch_bounds__(256, 2) void pyr_fast_kernel(FastArgs A) {
   float* const gimg = A.gpyr + b * A.g_img;
   const long long plane_bytes = (long long)A.rows * A.pitch * 4;
   const Rsrc rs0 = plane_rsrc(gimg + A.off[0], plane_bytes);
-  const FastCoefs& K = A.coef;
+  const KArgs KA = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();  // A, in the argument segment
   const int rbase = y0 - 64;  // ring slot of row y: (y - rbase) mod M; rows used >= y0 - 60
 
   const float* img = OCT0 ? A.src + b * A.s_img : nullptr;
   const float* prev = OCT0 ? nullptr : A.src + b * A.s_img + A.src_off;
-  float4 pre[2];
-  float gv[kGather];
+  Pre P;
   const int Zbeg = y0 - kLead, Zend = y1 + kH;
   if (OCT0) {
-    // prologue: row-pass rows [Zbeg-4, Zbeg+4)
-    fetch_image<VEC>(A, img, x0, Zbeg - 4, pre);
-    put_image(A, stage4, pre, x0, Zbeg - 4);
+    // prologue: row-pass rows [Zbeg-4, Zbeg+4), then stage step 0's image rows
+    fetch_image<VEC>(A, img, x0, Zbeg - 4, P);
+    SIFT_VM_WAIT(0);
+    put_image<VEC>(A, stage4, P, x0, Zbeg - 4);
     __syncthreads();
-    hb_pass(stage4, hb4, K.base, Zbeg - 4);
-    fetch_image<VEC>(A, img, x0, Zbeg + 4, pre);
+    hb_pass(stage4, hb4, fresh(KA)->coef.base, Zbeg - 4);
+    __syncthreads();
+    fetch_image<VEC>(A, img, x0, Zbeg + 4, P);
+    SIFT_VM_WAIT(0);
+    put_image<VEC>(A, stage4, P, x0, Zbeg + 4);
   } else {
     for (int c = t; c < kBW; c += 256) {
       const int x = x0 - kH + c;
@@ -378,81 +503,93 @@ __global__ __launch_bounds__(256, 2) void pyr_fast_kernel(FastArgs A) {
       xmap[c] = sx;
     }
     __syncthreads();
-    fetch_decim(A, prev, xmap, Zbeg, gv);
+    fetch_decim(A, prev, xmap, Zbeg, P);
+    SIFT_VM_WAIT(0);
+    put_decim(A, stage, rs0, xmap, P, Zbeg, x0, y0, y1);
   }
-  // 16 dropped stores: the loop enters with as many VMEM ops behind the
-  // prefetch as a step's column passes leave, so hipcc's wait for it at the
-  // top of the loop is vmcnt(16+) on every path instead of vmcnt(0).
-#pragma unroll
-  for (int k = 0; k < 16; ++k) st_plane(rs0, kDrop, 0.f);
-  __syncthreads();
 
-  const int ht = t & 127;
-  const int hr = ht >> 4, hj = ht & 15;  // row-pass item: base row hr, columns [8hj, 8hj+8)
-  const int x = x0 + ht;                 // column-pass item
-  const bool colok = x < C;
+  // wave roles: row passes 0, 1: sigma 4 + sigma 1, 2, 3: sigma 3 + sigma 2
+  // (lanes of a pair of waves: row pair hs, 4-column group hj); column passes
+  // 0, 1: sigma 4 + sigma 1, rows [0, 4) / [4, 8) of the step, 2: sigma 3,
+  // 3: sigma 2 (lane: columns xc, xc+1) -- 136 to 200 packed FMAs per lane.
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int L = t & 127;
+  const int hs = ((L >> 4) & 1) | ((L >> 6) << 1);
+  const int hj = (L & 15) | (((L >> 5) & 1) << 4);
+  const int lane = t & 63;
+  const int xc = x0 + 2 * lane;
+  const bool colok = xc < C;
   for (int Z = Zbeg; Z < Zend; Z += kRB) {
-    // ---- base rows [Z, Z+8) ----
+    __syncthreads();  // this step's staged image rows (octave 0) / base rows are published
+    // ---- octave 0: base rows [Z, Z+8) from the staged image rows ----
     if (OCT0) {
-      put_image(A, stage4, pre, x0, Z + 4);
+      hb_pass(stage4, hb4, fresh(KA)->coef.base, Z + 4);
       __syncthreads();
-      hb_pass(stage4, hb4, K.base, Z + 4);
-      __syncthreads();
-      if (t < kBW) {
+      if (t < kBW / 2) {
         if (Z & 8)
-          base_col<4>(A, hb, stage, rs0, t, Z, x0, y0, y1);
+          base_col<4>(A, fresh(KA)->coef.base, hb, stage4, rs0, t, Z, x0, y0, y1);
         else
-          base_col<12>(A, hb, stage, rs0, t, Z, x0, y0, y1);
+          base_col<12>(A, fresh(KA)->coef.base, hb, stage4, rs0, t, Z, x0, y0, y1);
       }
-    } else {
-#pragma unroll
-      for (int u = 0; u < kGather; ++u) {
-        const int i = t + 256 * u;
-        if (i < kRB * kBW) {
-          const int r = i / kBW, c = i - r * kBW;
-          const int y = Z + r;
-          const bool ok = y >= 0 && y < A.rows && xmap[c] >= 0;
-          put_base(A, stage, rs0, r, c, y, x0 - kH + c, y0, y1, ok ? gv[u] : 0.f);
-        }
-      }
-    }
-    __syncthreads();
-    // next step's source rows, in flight during this step's passes
-    if (Z + kRB < Zend) {
-      if (OCT0)
-        fetch_image<VEC>(A, img, x0, Z + kRB + 4, pre);
-      else
-        fetch_decim(A, prev, xmap, Z + kRB, gv);
+      __syncthreads();
     }
     // ---- row passes: h rows [Z, Z+8) -> ring slots [(Z - rbase) mod M, +8) ----
-    if (!(A.ablate & 4)) {
-      if (t < 128) {
-        if (Z + kRB > y0 - 18 && Z < y1 + 18)
-          row_pass<18>(stage4, rings4, K.s4, hr, hj, (Z - rbase) % Ring<18>::M + hr);
-        if (Z + kRB > y0 - 4 && Z < y1 + 4)
-          row_pass<4>(stage4, rings4, K.s1, hr, hj, (Z - rbase) % Ring<4>::M + hr);
-      } else {
-        if (Z + kRB > y0 - 12 && Z < y1 + 12)
-          row_pass<12>(stage4, rings4, K.s3, hr, hj, (Z - rbase) % Ring<12>::M + hr);
-        if (Z + kRB > y0 - 8 && Z < y1 + 8)
-          row_pass<8>(stage4, rings4, K.s2, hr, hj, (Z - rbase) % Ring<8>::M + hr);
-      }
+    if (wv < 2) {
+      if (Z + kRB > y0 - 18 && Z < y1 + 18)
+        row_pass<18>(stage4, rings4, fresh(KA)->coef.s4, hs, hj, (Z - rbase) % Ring<18>::M + 2 * hs);
+      if (Z + kRB > y0 - 4 && Z < y1 + 4)
+        row_pass<4>(stage4, rings4, fresh(KA)->coef.s1, hs, hj, (Z - rbase) % Ring<4>::M + 2 * hs);
+    } else {
+      if (Z + kRB > y0 - 12 && Z < y1 + 12)
+        row_pass<12>(stage4, rings4, fresh(KA)->coef.s3, hs, hj, (Z - rbase) % Ring<12>::M + 2 * hs);
+      if (Z + kRB > y0 - 8 && Z < y1 + 8)
+        row_pass<8>(stage4, rings4, fresh(KA)->coef.s2, hs, hj, (Z - rbase) % Ring<8>::M + 2 * hs);
     }
     __syncthreads();
-    // ---- column passes: plane rows [Z - w, Z - w + 8), every step (fixed store count) ----
-    if (t < 128) {
-      col_pass<18, 0>(((Z - 36 - rbase) % Ring<18>::M) >> 3, rings, K.s4, ht,
-                      plane_rsrc(gimg + A.off[4], plane_bytes), A.pitch, x, Z, y0, y1, colok);
-      col_pass<4, 0>(((Z - 8 - rbase) % Ring<4>::M) >> 3, rings, K.s1, ht,
-                     plane_rsrc(gimg + A.off[1], plane_bytes), A.pitch, x, Z, y0, y1, colok);
+    // next step's source values, in flight during the column passes
+    const bool more = Z + kRB < Zend;
+    if (more) {
+      if (OCT0)
+        fetch_image<VEC>(A, img, x0, Z + kRB + 4, P);
+      else
+        fetch_decim(A, prev, xmap, Z + kRB, P);
+    }
+    // ---- column passes: plane rows [Z - w, Z - w + 8) ----
+    // Every wave issues exactly 8 stores after the prefetch, so one
+    // vmcnt(8) after the join waits for the prefetch and nothing else.
+    if (wv < 2) {
+      const Rsrc rs4 = plane_rsrc(gimg + A.off[4], plane_bytes);
+      const Rsrc rs1 = plane_rsrc(gimg + A.off[1], plane_bytes);
+      if (wv == 0) {
+        col_pass<18, 4, 0, 0>(col_slot<18, 0>(Z, rbase), rings, fresh(KA)->coef.s4, lane, rs4, A.pitch, xc, Z, y0,
+                              y1, colok);
+        col_pass<4, 4, 0, 0>(col_slot<4, 0>(Z, rbase), rings, fresh(KA)->coef.s1, lane, rs1, A.pitch, xc, Z, y0, y1,
+                             colok);
+      } else {
+        col_pass<18, 4, 4, 0>(col_slot<18, 4>(Z, rbase), rings, fresh(KA)->coef.s4, lane, rs4, A.pitch, xc, Z, y0,
+                              y1, colok);
+        col_pass<4, 4, 4, 0>(col_slot<4, 4>(Z, rbase), rings, fresh(KA)->coef.s1, lane, rs1, A.pitch, xc, Z, y0, y1,
+                             colok);
+      }
+    } else if (wv == 2) {
+      col_pass<12, 8, 0, 0>(col_slot<12, 0>(Z, rbase), rings, fresh(KA)->coef.s3, lane,
+                            plane_rsrc(gimg + A.off[3], plane_bytes), A.pitch, xc, Z, y0, y1, colok);
     } else {
-      col_pass<12, 0>(((Z - 24 - rbase) % Ring<12>::M) >> 3, rings, K.s3, ht,
-                      plane_rsrc(gimg + A.off[3], plane_bytes), A.pitch, x, Z, y0, y1, colok);
-      col_pass<8, 0>(((Z - 16 - rbase) % Ring<8>::M) >> 3, rings, K.s2, ht,
-                     plane_rsrc(gimg + A.off[2], plane_bytes), A.pitch, x, Z, y0, y1, colok);
+      col_pass<8, 8, 0, 0>(col_slot<8, 0>(Z, rbase), rings, fresh(KA)->coef.s2, lane,
+                           plane_rsrc(gimg + A.off[2], plane_bytes), A.pitch, xc, Z, y0, y1, colok);
+    }
+    if (more) SIFT_VM_WAIT(8);
+    // stage the next step's source (the row passes are done with this step's base rows)
+    if (more) {
+      if (OCT0)
+        put_image<VEC>(A, stage4, P, x0, Z + kRB + 4);
+      else
+        put_decim(A, stage, rs0, xmap, P, Z + kRB, x0, y0, y1);
     }
   }
 }
+
+#undef SIFT_VM_WAIT
 
 // 1-D taps of sigma: g(a) = exp(-a^2 / (2 sigma^2)) / sqrt(2 pi sigma^2), the
 // square root of the 2-D kernel's normalisation (src/sift.cpp:103, same
@@ -465,6 +602,8 @@ void fast_taps(float sigma, float* g) {
 }
 
 }  // namespace
+
+
 
 size_t fast_coefs_size() { return sizeof(FastCoefs); }
 
@@ -525,8 +664,6 @@ void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Pl
   ch = (ch + kRB - 1) / kRB * kRB;
   chunks = (O.rows + ch - 1) / ch;
   A.chunk = ch;
-  static const int ablate = getenv("SIFT_FAST_ABLATE") ? atoi(getenv("SIFT_FAST_ABLATE")) : 0;
-  A.ablate = ablate;
   dim3 grid(strips, chunks, batch);
   if (o > 0)
     hipLaunchKernelGGL((pyr_fast_kernel<false, false>), grid, dim3(256), 0, st, A);
