@@ -28,8 +28,7 @@
 //    registers straight from LDS: row passes pair two rows (the base / image
 //    rows are staged row-pair interleaved, so one ds_read_b128 yields two
 //    columns of two rows), column passes pair two columns (ds_read_b64);
-//  * the taps come from the kernel-argument segment with scalar loads issued
-//    per pass (fresh()), not held in SGPRs across the loop (spills);
+//  * the taps sit in VGPRs for the whole walk, one per tap (pk_tap);
 //  * the next step's source rows are loaded during the column passes with
 //    loads hipcc does not track and waited for with an explicit vmcnt (see
 //    ld2_async); every load is branch-free (clamped address, the padding
@@ -84,7 +83,6 @@ static_assert(2 * kLds0 * 4 <= 160 * 1024, "two workgroups per CU");
 static_assert(kGather == 6, "SIFT_VM_WAIT operand list");
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
-typedef const __attribute__((address_space(4))) float* Taps;  // see fresh()
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
@@ -116,11 +114,34 @@ __device__ __forceinline__ void lds_bases(const f2* p, LdsF2 (&b)[NB]) {
   }
 }
 
-// Two independent fmaf in one v_pk_fma_f32; each element is still the same
-// sequential fmaf chain as the scalar form.
-__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 __device__ __forceinline__ f2 splat(float k) { return f2{k, k}; }
+
+// acc + a * g_b with the taps held in VGPRs as pairs g[j] = (g_2j, g_2j+1):
+// op_sel picks tap b out of its pair for both halves, so a tap costs one VGPR
+// and no copy.  (As SGPR operands all 97 taps spilled; loaded per pass from
+// the argument segment, the scalar loads made every pass wait lgkmcnt(0) for
+// its whole LDS window; as (k, k) pairs in LDS the broadcast reads doubled
+// the LDS cycles.)  The FMA loops below issue 4 or 8 independent chains, so
+// dependent pk_fma are never adjacent.
+__device__ __forceinline__ f2 pk_tap(f2 a, const f2* g, int b, f2 c) {
+  f2 d;
+  if (b & 1)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(d) : "v"(a), "v"(g[b >> 1]), "v"(c));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(g[b >> 1]), "v"(c));
+  return d;
+}
+
+// Taps of half-width W as VGPR pairs (see pk_tap).
+template <int W>
+__device__ __forceinline__ void tap_pairs(const __attribute__((address_space(4))) float* k, f2 (&g)[W + 1]) {
+#pragma unroll
+  for (int j = 0; j <= W; ++j) {
+    g[j] = f2{k[2 * j], 2 * j + 1 <= 2 * W ? k[2 * j + 1] : 0.f};
+    asm volatile("" : "+v"(g[j]));
+  }
+}
 
 // Row pass of one scale for base rows (2s, 2s+1) and output columns
 // [4j, 4j+4): h[Z + 2s + e][4j + i] = sum_b g[b] base[2s + e][4j + i + 18 - W + b].
@@ -131,7 +152,7 @@ __device__ __forceinline__ f2 splat(float k) { return f2{k, k}; }
 // are distinct (conflict free).  The two output rows are written with
 // ds_write_b128 (8 contiguous lanes per group: conflict free).
 template <int W>
-__device__ __forceinline__ void row_pass(const float4* __restrict__ bs4, float4* __restrict__ rings4, Taps g,
+__device__ __forceinline__ void row_pass(const float4* __restrict__ bs4, float4* __restrict__ rings4, const f2* g,
                                          int s, int j, int slot) {
   constexpr int C0 = kH - W, NW = 4 + 2 * W;
   static_assert(C0 % 2 == 0 && NW % 2 == 0, "windows start on a column pair");
@@ -148,9 +169,8 @@ __device__ __forceinline__ void row_pass(const float4* __restrict__ bs4, float4*
   for (int i = 0; i < 4; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int b = 0; b <= 2 * W; ++b) {
-    const f2 k = splat(g[b]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = pk_fma(w[i + b], k, acc[i]);
+    for (int i = 0; i < 4; ++i) acc[i] = pk_tap(w[i + b], g, b, acc[i]);
   }
   // slot + 1 never wraps: slot = (Z - rbase) mod M + 2s with Z - rbase and M
   // multiples of 8.
@@ -166,7 +186,7 @@ __device__ __forceinline__ void row_pass(const float4* __restrict__ bs4, float4*
 // are dropped (a pair that straddles an odd image width also writes the pitch
 // padding column, which nothing reads).
 template <int W, int S0, int NR>
-__device__ __forceinline__ void col_fixed(const float* __restrict__ rings, Taps g, int lane, Rsrc rs, int pitch,
+__device__ __forceinline__ void col_fixed(const float* __restrict__ rings, const f2* g, int lane, Rsrc rs, int pitch,
                                           int x, int Y, int y0, int y1, bool colok) {
   constexpr int M = Ring<W>::M, N = NR + 2 * W;
   LdsF2 ring[4];
@@ -179,9 +199,8 @@ __device__ __forceinline__ void col_fixed(const float* __restrict__ rings, Taps 
   for (int i = 0; i < NR; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int a = 0; a <= 2 * W; ++a) {
-    const f2 k = splat(g[a]);
 #pragma unroll
-    for (int i = 0; i < NR; ++i) acc[i] = pk_fma(win[i + a], k, acc[i]);
+    for (int i = 0; i < NR; ++i) acc[i] = pk_tap(win[i + a], g, a, acc[i]);
   }
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
@@ -198,7 +217,7 @@ __device__ __forceinline__ void col_fixed(const float* __restrict__ rings, Taps 
 // s0 = (Z - 2W + R - rbase) mod M = 8c + R0 with R0 = (R - 2W) mod 8 (steps
 // and rbase are multiples of 8): uniform dispatch to the body for c.
 template <int W, int NR, int R, int C>
-__device__ __forceinline__ void col_pass(int c, const float* __restrict__ rings, Taps g, int lane, Rsrc rs,
+__device__ __forceinline__ void col_pass(int c, const float* __restrict__ rings, const f2* g, int lane, Rsrc rs,
                                          int pitch, int x, int Z, int y0, int y1, bool colok) {
   constexpr int R0 = (((R - 2 * W) % 8) + 8) % 8;
   if constexpr (C + 1 < Ring<W>::M / 8) {
@@ -233,22 +252,12 @@ struct FastArgs {
   int pitch, rows, cols;
   int srows, scols;        // source (previous octave) shape
   int chunk;               // rows per workgroup (multiple of kRB)
-  FastCoefs coef;          // by value: read in the kernel through fresh()
+  FastCoefs coef;          // by value: scalar loads from the argument segment
 };
 
 namespace {
 
-// The taps are read from the kernel-argument segment (scalar loads that no
-// plane store can alias) through a pointer made opaque at each pass, so hipcc
-// loads each pass's taps right before the pass instead of keeping all 97 live
-// across the step loop (which spilled ~290 SGPRs to VGPR lanes and cost a
-// v_readlane per tap use).
-typedef const __attribute__((address_space(4))) FastArgs* KArgs;
-
-__device__ __forceinline__ KArgs fresh(KArgs p) {
-  asm volatile("" : "+s"(p));
-  return p;
-}
+typedef const __attribute__((address_space(4))) FastArgs* KArgs;  // A in the argument segment
 
 // Source prefetch with loads the compiler does not track (inline asm).  With
 // ordinary loads hipcc counted VMEM operations conservatively across the
@@ -387,7 +396,7 @@ __device__ __forceinline__ void put_decim(const FastArgs& A, float* __restrict__
 // [0, 164) (column c <-> image column x0 - 18 + c); lane t < 164 does row pair
 // s = t / 41, columns [4j, 4j+4), j = t % 41, from staged columns
 // [4j+2, 4j+14).
-__device__ __forceinline__ void hb_pass(const float4* __restrict__ stage4, float4* __restrict__ hb4, Taps g,
+__device__ __forceinline__ void hb_pass(const float4* __restrict__ stage4, float4* __restrict__ hb4, const f2* g,
                                         int Y) {
   const int t = threadIdx.x;
   if (t >= 4 * 41) return;
@@ -405,9 +414,8 @@ __device__ __forceinline__ void hb_pass(const float4* __restrict__ stage4, float
   for (int i = 0; i < 4; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int b = 0; b < 9; ++b) {
-    const f2 k = splat(g[b]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = pk_fma(w[i + b], k, acc[i]);
+    for (int i = 0; i < 4; ++i) acc[i] = pk_tap(w[i + b], g, b, acc[i]);
   }
   hb4[((Y + 2 * s) & (kHbRows - 1)) * (kBP / 4) + j] = make_float4(acc[0].x, acc[1].x, acc[2].x, acc[3].x);
   hb4[((Y + 2 * s + 1) & (kHbRows - 1)) * (kBP / 4) + j] = make_float4(acc[0].y, acc[1].y, acc[2].y, acc[3].y);
@@ -420,7 +428,7 @@ __device__ __forceinline__ void hb_pass(const float4* __restrict__ stage4, float
 // rows.  c = 2p is even, so a pair is entirely inside or outside the strip's
 // output columns.
 template <int S0>
-__device__ __forceinline__ void base_col(const FastArgs& A, Taps g, const float* __restrict__ hb,
+__device__ __forceinline__ void base_col(const FastArgs& A, const f2* g, const float* __restrict__ hb,
                                          float4* __restrict__ bs4, Rsrc rs0, int p, int Z, int x0, int y0,
                                          int y1) {
   LdsF2 h2[4];  // see lds_bases (hb rows are 688 B apart)
@@ -433,9 +441,8 @@ __device__ __forceinline__ void base_col(const FastArgs& A, Taps g, const float*
   for (int i = 0; i < 8; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int a = 0; a < 9; ++a) {
-    const f2 k = splat(g[a]);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = pk_fma(win[i + a], k, acc[i]);
+    for (int i = 0; i < 8; ++i) acc[i] = pk_tap(win[i + a], g, a, acc[i]);
   }
   const int c = 2 * p, x = x0 - kH + c;
   const bool colout = c >= kH && c < kH + kFW && x < A.cols;
@@ -453,140 +460,165 @@ __device__ __forceinline__ void base_col(const FastArgs& A, Taps g, const float*
   asm volatile("; base_col %0" ::"n"(S0));  // see col_fixed
 }
 
-template <bool OCT0, bool VEC>
-__global__ __launch_bounds__(256, 2) void pyr_fast_kernel(FastArgs A) {
-  __shared__ float4 lds4[(OCT0 ? kLds0 : kLdsN) / 4];
-  float* const lds = reinterpret_cast<float*>(lds4);
-  float4* const stage4 = lds4;  // staged image row pairs (octave 0) / base row pairs
-  float* const stage = lds;
-  float4* const hb4 = lds4 + kStage / 4;  // octave 0 only
-  const float* const hb = lds + kStage;
-  float4* const rings4 = lds4 + (kStage + (OCT0 ? kHbRows * kBP : 0)) / 4;
-  const float* const rings = reinterpret_cast<const float*>(rings4);
-  int* const xmap = reinterpret_cast<int*>(lds + kStage + kRingRows * kRP);  // octave > 0 only
+// LDS carve-up and per-workgroup constants of the step walk.
+struct Walk {
+  float4* stage4;  // staged image row pairs (octave 0) / base row pairs
+  float4* hb4;     // octave-0 row-pass ring
+  float4* rings4;  // scale rings
+  int* xmap;       // octave > 0: decimation column map
+  float* gimg;     // this image's pyramid block
+  const float* img;   // octave 0: this image
+  const float* prev;  // octave > 0: the previous octave's scale-3 plane
+  long long plane_bytes;
+  Rsrc rs0;
+  int x0, y0, y1, rbase, Zbeg, Zend;
+};
 
+// The step walk of one wave role.  The waves of a workgroup split into two
+// roles that run their own copy of the loop (same barriers, so the
+// workgroup stays in step):
+//   role 0 (waves 0, 1): row and column passes of sigma 4 (W = 18) and sigma 1 (4)
+//   role 1 (waves 2, 3): row passes of sigma 3 (12) and sigma 2 (8), column
+//                        pass of sigma 3 (wave 2) / sigma 2 (wave 3)
+// so each wave's loop is about half the code.  Row passes: the lanes of a role's two waves cover row
+// pair hs x 4-column group hj; column passes: lane -> columns (xc, xc + 1).
+// Every wave issues exactly 8 plane stores in the column passes.
+template <bool OCT0, bool VEC, int WA, int WB>
+__device__ __forceinline__ void walk(const FastArgs& A, const Walk& K, int wv) {
+  const KArgs KA = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  f2 kb[5], ka[WA + 1], kc[WB + 1];
+  tap_pairs<4>(KA->coef.base, kb);
+  tap_pairs<WA>(WA == 18 ? KA->coef.s4 : KA->coef.s3, ka);
+  tap_pairs<WB>(WB == 4 ? KA->coef.s1 : KA->coef.s2, kc);
   const int t = threadIdx.x;
-  const int b = blockIdx.z;
-  const int x0 = blockIdx.x * kFW;
-  const int y0 = blockIdx.y * A.chunk;
-  const int y1 = min(y0 + A.chunk, A.rows);
-  const int C = A.cols;
-  float* const gimg = A.gpyr + b * A.g_img;
-  const long long plane_bytes = (long long)A.rows * A.pitch * 4;
-  const Rsrc rs0 = plane_rsrc(gimg + A.off[0], plane_bytes);
-  const KArgs KA = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();  // A, in the argument segment
-  const int rbase = y0 - 64;  // ring slot of row y: (y - rbase) mod M; rows used >= y0 - 60
-
-  const float* img = OCT0 ? A.src + b * A.s_img : nullptr;
-  const float* prev = OCT0 ? nullptr : A.src + b * A.s_img + A.src_off;
-  Pre P;
-  const int Zbeg = y0 - kLead, Zend = y1 + kH;
-  if (OCT0) {
-    // prologue: row-pass rows [Zbeg-4, Zbeg+4), then stage step 0's image rows
-    fetch_image<VEC>(A, img, x0, Zbeg - 4, P);
-    SIFT_VM_WAIT(0);
-    put_image<VEC>(A, stage4, P, x0, Zbeg - 4);
-    __syncthreads();
-    hb_pass(stage4, hb4, fresh(KA)->coef.base, Zbeg - 4);
-    __syncthreads();
-    fetch_image<VEC>(A, img, x0, Zbeg + 4, P);
-    SIFT_VM_WAIT(0);
-    put_image<VEC>(A, stage4, P, x0, Zbeg + 4);
-  } else {
-    for (int c = t; c < kBW; c += 256) {
-      const int x = x0 - kH + c;
-      int sx = -1;
-      if (x >= 0 && x < C) {
-        sx = (int)floor(x * A.ifx);
-        sx = sx < A.scols - 1 ? sx : A.scols - 1;
-      }
-      xmap[c] = sx;
-    }
-    __syncthreads();
-    fetch_decim(A, prev, xmap, Zbeg, P);
-    SIFT_VM_WAIT(0);
-    put_decim(A, stage, rs0, xmap, P, Zbeg, x0, y0, y1);
-  }
-
-  // wave roles: row passes 0, 1: sigma 4 + sigma 1, 2, 3: sigma 3 + sigma 2
-  // (lanes of a pair of waves: row pair hs, 4-column group hj); column passes
-  // 0, 1: sigma 4 + sigma 1, rows [0, 4) / [4, 8) of the step, 2: sigma 3,
-  // 3: sigma 2 (lane: columns xc, xc+1) -- 136 to 200 packed FMAs per lane.
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int L = t & 127;
   const int hs = ((L >> 4) & 1) | ((L >> 6) << 1);
   const int hj = (L & 15) | (((L >> 5) & 1) << 4);
   const int lane = t & 63;
-  const int xc = x0 + 2 * lane;
-  const bool colok = xc < C;
-  for (int Z = Zbeg; Z < Zend; Z += kRB) {
+  const int xc = K.x0 + 2 * lane;
+  const bool colok = xc < A.cols;
+  const int x0 = K.x0, y0 = K.y0, y1 = K.y1, rbase = K.rbase;
+  const float* rings = reinterpret_cast<const float*>(K.rings4);
+  float* stage = reinterpret_cast<float*>(K.stage4);
+  Pre P;
+  for (int Z = K.Zbeg; Z < K.Zend; Z += kRB) {
     __syncthreads();  // this step's staged image rows (octave 0) / base rows are published
     // ---- octave 0: base rows [Z, Z+8) from the staged image rows ----
     if (OCT0) {
-      hb_pass(stage4, hb4, fresh(KA)->coef.base, Z + 4);
+      hb_pass(K.stage4, K.hb4, kb, Z + 4);
       __syncthreads();
       if (t < kBW / 2) {
+        const float* hb = reinterpret_cast<const float*>(K.hb4);
         if (Z & 8)
-          base_col<4>(A, fresh(KA)->coef.base, hb, stage4, rs0, t, Z, x0, y0, y1);
+          base_col<4>(A, kb, hb, K.stage4, K.rs0, t, Z, x0, y0, y1);
         else
-          base_col<12>(A, fresh(KA)->coef.base, hb, stage4, rs0, t, Z, x0, y0, y1);
+          base_col<12>(A, kb, hb, K.stage4, K.rs0, t, Z, x0, y0, y1);
       }
       __syncthreads();
     }
     // ---- row passes: h rows [Z, Z+8) -> ring slots [(Z - rbase) mod M, +8) ----
-    if (wv < 2) {
-      if (Z + kRB > y0 - 18 && Z < y1 + 18)
-        row_pass<18>(stage4, rings4, fresh(KA)->coef.s4, hs, hj, (Z - rbase) % Ring<18>::M + 2 * hs);
-      if (Z + kRB > y0 - 4 && Z < y1 + 4)
-        row_pass<4>(stage4, rings4, fresh(KA)->coef.s1, hs, hj, (Z - rbase) % Ring<4>::M + 2 * hs);
-    } else {
-      if (Z + kRB > y0 - 12 && Z < y1 + 12)
-        row_pass<12>(stage4, rings4, fresh(KA)->coef.s3, hs, hj, (Z - rbase) % Ring<12>::M + 2 * hs);
-      if (Z + kRB > y0 - 8 && Z < y1 + 8)
-        row_pass<8>(stage4, rings4, fresh(KA)->coef.s2, hs, hj, (Z - rbase) % Ring<8>::M + 2 * hs);
-    }
+    if (Z + kRB > y0 - WA && Z < y1 + WA)
+      row_pass<WA>(K.stage4, K.rings4, ka, hs, hj, (Z - rbase) % Ring<WA>::M + 2 * hs);
+    if (Z + kRB > y0 - WB && Z < y1 + WB)
+      row_pass<WB>(K.stage4, K.rings4, kc, hs, hj, (Z - rbase) % Ring<WB>::M + 2 * hs);
     __syncthreads();
     // next step's source values, in flight during the column passes
-    const bool more = Z + kRB < Zend;
+    const bool more = Z + kRB < K.Zend;
     if (more) {
       if (OCT0)
-        fetch_image<VEC>(A, img, x0, Z + kRB + 4, P);
+        fetch_image<VEC>(A, K.img, x0, Z + kRB + 4, P);
       else
-        fetch_decim(A, prev, xmap, Z + kRB, P);
+        fetch_decim(A, K.prev, K.xmap, Z + kRB, P);
     }
     // ---- column passes: plane rows [Z - w, Z - w + 8) ----
-    // Every wave issues exactly 8 stores after the prefetch, so one
-    // vmcnt(8) after the join waits for the prefetch and nothing else.
-    if (wv < 2) {
-      const Rsrc rs4 = plane_rsrc(gimg + A.off[4], plane_bytes);
-      const Rsrc rs1 = plane_rsrc(gimg + A.off[1], plane_bytes);
+    if (WA == 18) {
+      const Rsrc rs4 = plane_rsrc(K.gimg + A.off[4], K.plane_bytes);
+      const Rsrc rs1 = plane_rsrc(K.gimg + A.off[1], K.plane_bytes);
       if (wv == 0) {
-        col_pass<18, 4, 0, 0>(col_slot<18, 0>(Z, rbase), rings, fresh(KA)->coef.s4, lane, rs4, A.pitch, xc, Z, y0,
-                              y1, colok);
-        col_pass<4, 4, 0, 0>(col_slot<4, 0>(Z, rbase), rings, fresh(KA)->coef.s1, lane, rs1, A.pitch, xc, Z, y0, y1,
-                             colok);
+        col_pass<18, 4, 0, 0>(col_slot<18, 0>(Z, rbase), rings, ka, lane, rs4, A.pitch, xc, Z, y0, y1, colok);
+        col_pass<4, 4, 0, 0>(col_slot<4, 0>(Z, rbase), rings, kc, lane, rs1, A.pitch, xc, Z, y0, y1, colok);
       } else {
-        col_pass<18, 4, 4, 0>(col_slot<18, 4>(Z, rbase), rings, fresh(KA)->coef.s4, lane, rs4, A.pitch, xc, Z, y0,
-                              y1, colok);
-        col_pass<4, 4, 4, 0>(col_slot<4, 4>(Z, rbase), rings, fresh(KA)->coef.s1, lane, rs1, A.pitch, xc, Z, y0, y1,
-                             colok);
+        col_pass<18, 4, 4, 0>(col_slot<18, 4>(Z, rbase), rings, ka, lane, rs4, A.pitch, xc, Z, y0, y1, colok);
+        col_pass<4, 4, 4, 0>(col_slot<4, 4>(Z, rbase), rings, kc, lane, rs1, A.pitch, xc, Z, y0, y1, colok);
       }
-    } else if (wv == 2) {
-      col_pass<12, 8, 0, 0>(col_slot<12, 0>(Z, rbase), rings, fresh(KA)->coef.s3, lane,
-                            plane_rsrc(gimg + A.off[3], plane_bytes), A.pitch, xc, Z, y0, y1, colok);
     } else {
-      col_pass<8, 8, 0, 0>(col_slot<8, 0>(Z, rbase), rings, fresh(KA)->coef.s2, lane,
-                           plane_rsrc(gimg + A.off[2], plane_bytes), A.pitch, xc, Z, y0, y1, colok);
+      if (wv == 2)
+        col_pass<12, 8, 0, 0>(col_slot<12, 0>(Z, rbase), rings, ka, lane, plane_rsrc(K.gimg + A.off[3], K.plane_bytes),
+                              A.pitch, xc, Z, y0, y1, colok);
+      else
+        col_pass<8, 8, 0, 0>(col_slot<8, 0>(Z, rbase), rings, kc, lane, plane_rsrc(K.gimg + A.off[2], K.plane_bytes),
+                             A.pitch, xc, Z, y0, y1, colok);
     }
-    if (more) SIFT_VM_WAIT(8);
     // stage the next step's source (the row passes are done with this step's base rows)
     if (more) {
+      SIFT_VM_WAIT(8);
       if (OCT0)
-        put_image<VEC>(A, stage4, P, x0, Z + kRB + 4);
+        put_image<VEC>(A, K.stage4, P, x0, Z + kRB + 4);
       else
-        put_decim(A, stage, rs0, xmap, P, Z + kRB, x0, y0, y1);
+        put_decim(A, stage, K.rs0, K.xmap, P, Z + kRB, x0, y0, y1);
     }
   }
+}
+
+template <bool OCT0, bool VEC>
+__global__ __launch_bounds__(256, 2) void pyr_fast_kernel(FastArgs A) {
+  __shared__ float4 lds4[(OCT0 ? kLds0 : kLdsN) / 4];
+  float* const lds = reinterpret_cast<float*>(lds4);
+  Walk K;
+  K.stage4 = lds4;
+  K.hb4 = lds4 + kStage / 4;
+  K.rings4 = lds4 + (kStage + (OCT0 ? kHbRows * kBP : 0)) / 4;
+  K.xmap = reinterpret_cast<int*>(lds + kStage + kRingRows * kRP);
+
+  const int t = threadIdx.x;
+  const int b = blockIdx.z;
+  K.x0 = blockIdx.x * kFW;
+  K.y0 = blockIdx.y * A.chunk;
+  K.y1 = min(K.y0 + A.chunk, A.rows);
+  K.gimg = A.gpyr + b * A.g_img;
+  K.plane_bytes = (long long)A.rows * A.pitch * 4;
+  K.rs0 = plane_rsrc(K.gimg + A.off[0], K.plane_bytes);
+  K.rbase = K.y0 - 64;  // ring slot of row y: (y - rbase) mod M; rows used >= y0 - 60
+  K.img = OCT0 ? A.src + b * A.s_img : nullptr;
+  K.prev = OCT0 ? nullptr : A.src + b * A.s_img + A.src_off;
+  K.Zbeg = K.y0 - kLead;
+  K.Zend = K.y1 + kH;
+  const int x0 = K.x0;
+
+  Pre P;
+  if (OCT0) {
+    // prologue: row-pass rows [Zbeg-4, Zbeg+4), then stage step 0's image rows
+    f2 kb[5];
+    tap_pairs<4>(((KArgs)__builtin_amdgcn_kernarg_segment_ptr())->coef.base, kb);
+    fetch_image<VEC>(A, K.img, x0, K.Zbeg - 4, P);
+    SIFT_VM_WAIT(0);
+    put_image<VEC>(A, K.stage4, P, x0, K.Zbeg - 4);
+    __syncthreads();
+    hb_pass(K.stage4, K.hb4, kb, K.Zbeg - 4);
+    __syncthreads();
+    fetch_image<VEC>(A, K.img, x0, K.Zbeg + 4, P);
+    SIFT_VM_WAIT(0);
+    put_image<VEC>(A, K.stage4, P, x0, K.Zbeg + 4);
+  } else {
+    for (int c = t; c < kBW; c += 256) {
+      const int x = x0 - kH + c;
+      int sx = -1;
+      if (x >= 0 && x < A.cols) {
+        sx = (int)floor(x * A.ifx);
+        sx = sx < A.scols - 1 ? sx : A.scols - 1;
+      }
+      K.xmap[c] = sx;
+    }
+    __syncthreads();
+    fetch_decim(A, K.prev, K.xmap, K.Zbeg, P);
+    SIFT_VM_WAIT(0);
+    put_decim(A, lds, K.rs0, K.xmap, P, K.Zbeg, x0, K.y0, K.y1);
+  }
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (wv < 2)
+    walk<OCT0, VEC, 18, 4>(A, K, wv);
+  else
+    walk<OCT0, VEC, 12, 8>(A, K, wv);
 }
 
 #undef SIFT_VM_WAIT

@@ -43,22 +43,25 @@ def main():
         L = s[start:s.index('.Lfunc_end', start)].split('\n')
         tag = re.search(r'ILb(\d)ELb(\d)', m.group(1)).group(0)
         waits = [i for i, l in enumerate(L) if re.search(r's_waitcnt vmcnt\(\d+\)', l)]
-        w0 = [i for i in waits if 'vmcnt(0)' in L[i]][-1]
-        loop_waits = [i for i in waits if i > w0]
-        loads = [i for i, l in enumerate(L) if re.search(r'global_load_dword', l) and w0 < i < loop_waits[0]]
+        loads = [i for i, l in enumerate(L) if re.search(r'global_load_dword', l)]
         n = 0
         for i in loads:
+            w = next(j for j in waits if j > i)  # the explicit wait that ends this load's flight
             d = regs(L[i].split()[1].rstrip(','))
-            for j in range(i + 1, loop_waits[-1]):
+            for j in range(i + 1, w):
                 line = L[j].strip()
-                if line.startswith(';') or 's_waitcnt vmcnt' in line:
+                if line.startswith(';'):
                     continue
                 if all_regs(line) & d:
                     n += 1
                     print(f'  {tag}: line {j} touches prefetch register of line {i}: {line}')
-        stores = sum('buffer_store' in L[j] for j in range(loads[-1], loop_waits[0]))
-        print(f'{tag}: {len(loads)} prefetch loads, waits {[L[i].strip() for i in loop_waits]}, '
-              f'{stores} store instructions in between (all paths), {n} violations')
+        groups = sorted(set(next(j for j in waits if j > i) for i in loads))
+        for w in groups:
+            first = min(i for i in loads if next(j for j in waits if j > i) == w)
+            stores = sum('buffer_store' in L[j] for j in range(first, w))
+            print(f'{tag}: loads at {[i for i in loads if next(j for j in waits if j > i) == w]} -> '
+                  f'{L[w].strip()} at {w}, {stores} store instructions in between (all paths)')
+        print(f'{tag}: {n} violations')
         bad += n
     sys.exit(1 if bad else 0)
 
