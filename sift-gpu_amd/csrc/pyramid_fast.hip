@@ -516,13 +516,8 @@ __device__ __forceinline__ void walk(const FastArgs& A, const Walk& K, int wv) {
       }
       __syncthreads();
     }
-    // ---- row passes: h rows [Z, Z+8) -> ring slots [(Z - rbase) mod M, +8) ----
-    if (Z + kRB > y0 - WA && Z < y1 + WA)
-      row_pass<WA>(K.stage4, K.rings4, ka, hs, hj, (Z - rbase) % Ring<WA>::M + 2 * hs);
-    if (Z + kRB > y0 - WB && Z < y1 + WB)
-      row_pass<WB>(K.stage4, K.rings4, kc, hs, hj, (Z - rbase) % Ring<WB>::M + 2 * hs);
-    __syncthreads();
-    // next step's source values, in flight during the column passes
+    // next step's source values, in flight during the row and column passes
+    // (after the base stores, so exactly the 8 column-pass stores follow them)
     const bool more = Z + kRB < K.Zend;
     if (more) {
       if (OCT0)
@@ -530,6 +525,12 @@ __device__ __forceinline__ void walk(const FastArgs& A, const Walk& K, int wv) {
       else
         fetch_decim(A, K.prev, K.xmap, Z + kRB, P);
     }
+    // ---- row passes: h rows [Z, Z+8) -> ring slots [(Z - rbase) mod M, +8) ----
+    if (Z + kRB > y0 - WA && Z < y1 + WA)
+      row_pass<WA>(K.stage4, K.rings4, ka, hs, hj, (Z - rbase) % Ring<WA>::M + 2 * hs);
+    if (Z + kRB > y0 - WB && Z < y1 + WB)
+      row_pass<WB>(K.stage4, K.rings4, kc, hs, hj, (Z - rbase) % Ring<WB>::M + 2 * hs);
+    __syncthreads();
     // ---- column passes: plane rows [Z - w, Z - w + 8) ----
     if (WA == 18) {
       const Rsrc rs4 = plane_rsrc(K.gimg + A.off[4], K.plane_bytes);

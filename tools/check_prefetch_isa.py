@@ -45,22 +45,41 @@ def main():
         waits = [i for i, l in enumerate(L) if re.search(r's_waitcnt vmcnt\(\d+\)', l)]
         loads = [i for i, l in enumerate(L) if re.search(r'global_load_dword', l)]
         n = 0
+        labels = {l.split(':')[0]: k for k, l in enumerate(L) if re.match(r'^\.LBB\d+_\d+:', l)}
+
+        def flight(i):
+            """Lines a load's destination stays in flight over, up to its wait.
+            A rotated loop puts the loads after the wait: follow the first
+            backward branch after the load to its header."""
+            w = next((j for j in waits if j > i), None)
+            if w is not None:
+                return w, list(range(i + 1, w))
+            for k in range(i + 1, len(L)):
+                m2 = re.match(r'\s+s_c?branch\w*\s+(\.LBB\d+_\d+)', L[k])
+                if m2 and labels.get(m2.group(1), len(L)) < i:
+                    h = labels[m2.group(1)]
+                    w = next(j for j in waits if j > h)
+                    return w, list(range(i + 1, k + 1)) + list(range(h, w))
+            raise RuntimeError(f'{tag}: no wait for the load at line {i}')
+
         for i in loads:
-            w = next(j for j in waits if j > i)  # the explicit wait that ends this load's flight
+            w, span = flight(i)
             d = regs(L[i].split()[1].rstrip(','))
-            for j in range(i + 1, w):
+            for j in span:
                 line = L[j].strip()
                 if line.startswith(';'):
                     continue
                 if all_regs(line) & d:
                     n += 1
                     print(f'  {tag}: line {j} touches prefetch register of line {i}: {line}')
-        groups = sorted(set(next(j for j in waits if j > i) for i in loads))
-        for w in groups:
-            first = min(i for i in loads if next(j for j in waits if j > i) == w)
-            stores = sum('buffer_store' in L[j] for j in range(first, w))
-            print(f'{tag}: loads at {[i for i in loads if next(j for j in waits if j > i) == w]} -> '
-                  f'{L[w].strip()} at {w}, {stores} store instructions in between (all paths)')
+        groups = {}
+        for i in loads:
+            w, span = flight(i)
+            groups.setdefault(w, []).append((i, span))
+        for w, ls in sorted(groups.items()):
+            stores = sum('buffer_store' in L[j] for j in ls[0][1])
+            print(f'{tag}: loads at {[i for i, _ in ls]} -> {L[w].strip()} at {w}, '
+                  f'{stores} store instructions in between (all paths)')
         print(f'{tag}: {n} violations')
         bad += n
     sys.exit(1 if bad else 0)
