@@ -139,6 +139,21 @@ int sift_find_scale_space_extrema(sift_ctx* ctx, const float* gpyr, const float*
 int sift_calc_descriptors(sift_ctx* ctx, const float* gpyr, int rows, int cols, int n_octaves,
                           const sift_keypoint* kpts, int n, float* desc, int first_octave);
 
+/* ---- matching ------------------------------------------ */
+/* Replaces `BFMatcher(NORM_L1).knnMatch(query, train, matches, k)` of the
+ * reference application (src/main.cpp:25-27; the 0.86 ratio test at :28-40
+ * stays with the caller).  query [n_query][128], train [n_train][128] floats;
+ * for each query the k (1 or 2) nearest train rows by float L1 distance
+ * (OpenCV normL1_ summation order, see match.hip), ascending, an earlier train
+ * index first at equal distance.  idx / dist are [n_query][k]; when
+ * n_train < k the missing entries are idx -1, dist +inf.
+ * Host buffers (synchronous): */
+int sift_knn_match_l1(sift_ctx* ctx, const float* query, int n_query, const float* train, int n_train, int k,
+                      int* idx, float* dist);
+/* Device buffers (16-byte aligned rows), enqueued on the context's stream: */
+int sift_knn_match_l1_device(sift_ctx* ctx, const float* d_query, int n_query, const float* d_train,
+                             int n_train, int k, int* d_idx, float* d_dist);
+
 /* ---- self-test ------------------------------------------------------------ */
 /* Evaluates one device arithmetic helper element-wise on host arrays (n
  * values), for bit-exact checks of the GPU math against the CPU oracle:

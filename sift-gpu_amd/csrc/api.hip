@@ -76,9 +76,9 @@ struct StageRec {
 
 const char* const kStageNames[] = {"blur_base", "blur_octave", "decimate", "dog", "extrema",
                                    "refine_orient", "emit", "descriptor", "upload", "download",
-                                   "blur_1d", "pyramid_fast"};
+                                   "blur_1d", "pyramid_fast", "match"};
 enum Stage { ST_BLUR_BASE, ST_BLUR_OCT, ST_DECIMATE, ST_DOG, ST_EXTREMA, ST_REFINE, ST_EMIT,
-             ST_DESC, ST_UPLOAD, ST_DOWNLOAD, ST_BLUR1D, ST_PYR_FAST, ST_N };
+             ST_DESC, ST_UPLOAD, ST_DOWNLOAD, ST_BLUR1D, ST_PYR_FAST, ST_MATCH, ST_N };
 
 template <typename T>
 hipError_t dmalloc(T** p, size_t count) {
@@ -120,6 +120,8 @@ struct sift_ctx {
   int last_n = -1;                // keypoints held from the last host call
   bool last_has_desc = false;
   int* d_err = nullptr;
+  void* d_match = nullptr;        // knn-match scratch (grown on demand)
+  size_t match_cap = 0;
   // profiling
   std::vector<StageRec> recs;
   std::vector<hipEvent_t> pool;
@@ -492,7 +494,7 @@ int sift_ctx_destroy(sift_ctx* c) {
   void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
                   c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->d_img_off,
-                  c->d_kpts, c->d_desc, c->d_err};
+                  c->d_kpts, c->d_desc, c->d_err, c->d_match};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -814,6 +816,97 @@ int sift_selftest_math(sift_ctx* c, int op, const float* a, const float* b, floa
   (void)hipFree(db);
   (void)hipFree(dout);
   if (e != hipSuccess) return hip_fail(c, e, "sift_selftest_math");
+  return SIFT_OK;
+}
+
+// ---- BFMatcher(NORM_L1).knnMatch, src/main.cpp:25-27 ----
+namespace {
+
+int ensure_match(sift_ctx* c, size_t bytes) {
+  if (bytes <= c->match_cap) return SIFT_OK;
+  if (c->d_match) {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(c->d_match);
+    c->d_match = nullptr;
+    c->match_cap = 0;
+  }
+  if (hipMalloc(&c->d_match, bytes) != hipSuccess) return fail(c, SIFT_E_NOMEM, "match scratch");
+  c->match_cap = bytes;
+  return SIFT_OK;
+}
+
+size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+int check_match_args(sift_ctx* c, int n_query, int n_train, int k) {
+  if (n_query < 0 || n_train < 0) return fail(c, SIFT_E_INVALID, "negative descriptor count");
+  if (k != 1 && k != 2) return fail(c, SIFT_E_INVALID, "k must be 1 or 2");
+  return SIFT_OK;
+}
+
+size_t match_part_bytes(int nq, int nt) {
+  const size_t part = (size_t)knn_splits(nq, nt) * nq;
+  return align256(part * sizeof(float2)) + align256(part * sizeof(int2));
+}
+
+// Partials at d_match + off (the scratch must already hold off + match_part_bytes).
+int knn_device(sift_ctx* c, const float* q, int nq, const float* t, int nt, int k, int* idx, float* dist,
+               size_t off) {
+  const int splits = knn_splits(nq, nt);
+  const size_t part = (size_t)splits * nq;
+  char* base = static_cast<char*>(c->d_match) + off;
+  float2* pd = reinterpret_cast<float2*>(base);
+  int2* pi = reinterpret_cast<int2*>(base + align256(part * sizeof(float2)));
+  {
+    StageScope s(c, ST_MATCH, 2.0 * kDescLen * nq * (double)nt, 512.0 * (nq + (double)nt));
+    launch_knn_l1(c->stream, q, nq, t, nt, k, splits, pd, pi, idx, dist);
+  }
+  HIP_TRY(c, hipGetLastError());
+  return SIFT_OK;
+}
+
+}  // namespace
+
+int sift_knn_match_l1_device(sift_ctx* c, const float* d_query, int n_query, const float* d_train, int n_train,
+                             int k, int* d_idx, float* d_dist) {
+  if (!c) return SIFT_E_INVALID;
+  int rc = check_match_args(c, n_query, n_train, k);
+  if (rc) return rc;
+  if (n_query == 0) return SIFT_OK;
+  if (!d_query || !d_idx || !d_dist || (n_train > 0 && !d_train)) return fail(c, SIFT_E_INVALID, "null buffer");
+  if ((reinterpret_cast<uintptr_t>(d_query) | reinterpret_cast<uintptr_t>(d_train)) & 15)
+    return fail(c, SIFT_E_INVALID, "descriptor rows must be 16-byte aligned");
+  (void)hipSetDevice(c->device);
+  if ((rc = ensure_match(c, match_part_bytes(n_query, n_train)))) return rc;
+  return knn_device(c, d_query, n_query, d_train, n_train, k, d_idx, d_dist, 0);
+}
+
+int sift_knn_match_l1(sift_ctx* c, const float* query, int n_query, const float* train, int n_train, int k,
+                      int* idx, float* dist) {
+  if (!c) return SIFT_E_INVALID;
+  int rc = check_match_args(c, n_query, n_train, k);
+  if (rc) return rc;
+  if (n_query == 0) return SIFT_OK;
+  if (!query || !idx || !dist || (n_train > 0 && !train)) return fail(c, SIFT_E_INVALID, "null buffer");
+  (void)hipSetDevice(c->device);
+  const size_t qb = align256((size_t)n_query * kDescLen * sizeof(float));
+  const size_t tb = align256((size_t)(n_train ? n_train : 1) * kDescLen * sizeof(float));
+  const size_t ib = align256((size_t)n_query * k * sizeof(int)), db = align256((size_t)n_query * k * sizeof(float));
+  const size_t off = qb + tb + ib + db;
+  if ((rc = ensure_match(c, off + match_part_bytes(n_query, n_train)))) return rc;
+  char* base = static_cast<char*>(c->d_match);
+  float* dq = reinterpret_cast<float*>(base);
+  float* dt = reinterpret_cast<float*>(base + qb);
+  int* di = reinterpret_cast<int*>(base + qb + tb);
+  float* dd = reinterpret_cast<float*>(base + qb + tb + ib);
+  HIP_TRY(c, hipMemcpyAsync(dq, query, (size_t)n_query * kDescLen * sizeof(float), hipMemcpyHostToDevice,
+                            c->stream));
+  if (n_train)
+    HIP_TRY(c, hipMemcpyAsync(dt, train, (size_t)n_train * kDescLen * sizeof(float), hipMemcpyHostToDevice,
+                              c->stream));
+  if ((rc = knn_device(c, dq, n_query, dt, n_train, k, di, dd, off))) return rc;
+  HIP_TRY(c, hipMemcpyAsync(idx, di, (size_t)n_query * k * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(dist, dd, (size_t)n_query * k * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return SIFT_OK;
 }
 

@@ -96,6 +96,8 @@ def lib():
             "sift_calc_descriptors": (ip, [vp, fp, ip, ip, ip, vp, ip, fp, ip]),
             "sift_get_stage_stats": (ip, [vp, ctypes.POINTER(StageStat), ip, pint, ip]),
             "sift_selftest_math": (ip, [vp, ip, fp, fp, fp, ip]),
+            "sift_knn_match_l1": (ip, [vp, fp, ip, fp, ip, ip, pint, fp]),
+            "sift_knn_match_l1_device": (ip, [vp, vp, ip, vp, ip, ip, vp, vp]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -259,6 +261,26 @@ class Context:
                                                   _fp(desc), firstOctave))
         return desc
 
+    def knnMatch(self, query: np.ndarray, train: np.ndarray, k: int = 2):
+        """BFMatcher(NORM_L1).knnMatch as arrays (src/main.cpp:25-27): idx, dist
+        [n_query, k]; idx -1 / dist +inf where there are fewer than k train rows."""
+        q = np.ascontiguousarray(query, np.float32).reshape(-1, DESC_LEN)
+        t = np.ascontiguousarray(train, np.float32).reshape(-1, DESC_LEN)
+        idx = np.empty((len(q), k), np.int32)
+        dist = np.empty((len(q), k), np.float32)
+        self._check("sift_knn_match_l1",
+                    self._L.sift_knn_match_l1(self.h, _fp(q), len(q), _fp(t), len(t), k,
+                                              idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _fp(dist)))
+        return idx, dist
+
+    def knn_match_device(self, query_ptr: int, n_query: int, train_ptr: int, n_train: int, k: int,
+                         idx_ptr: int, dist_ptr: int):
+        """Device-pointer form, enqueued on the context stream (no sync)."""
+        self._check("sift_knn_match_l1_device",
+                    self._L.sift_knn_match_l1_device(self.h, ctypes.c_void_p(query_ptr), n_query,
+                                                     ctypes.c_void_p(train_ptr), n_train, k,
+                                                     ctypes.c_void_p(idx_ptr), ctypes.c_void_p(dist_ptr)))
+
     # ---- device batch API ------------------------------------------------
     def synth_images(self, out_ptr: int, batch: int, rows: int, cols: int, row_stride: int,
                      img_stride: int, seed_base: int = 0):
@@ -332,3 +354,42 @@ def findScaleSpaceExtrema(gpyr, dogpyr, nOctaves=5):
 
 def calDescriptor(gpyr, keypoints, firstOctave=0):
     return _ctx(*gpyr[0].shape).calDescriptor(gpyr, keypoints, firstOctave)
+
+
+# ---- matcher: the reference application's consumer ------
+class DMatch:
+    """cv::DMatch fields (queryIdx, trainIdx, imgIdx, distance)."""
+    __slots__ = ("queryIdx", "trainIdx", "imgIdx", "distance")
+
+    def __init__(self, queryIdx, trainIdx, imgIdx, distance):
+        self.queryIdx, self.trainIdx, self.imgIdx, self.distance = queryIdx, trainIdx, imgIdx, distance
+
+    def __repr__(self):
+        return f"DMatch({self.queryIdx}, {self.trainIdx}, {self.imgIdx}, {self.distance!r})"
+
+
+NORM_L1 = 2  # cv::NORM_L1
+
+
+class BFMatcher:
+    """`cv::BFMatcher(NORM_L1)` as the reference uses it (src/main.cpp:25-27):
+    knnMatch(queryDescriptors, trainDescriptors, k) -> per query a list of up to
+    k DMatch, nearest first.  Only NORM_L1 float descriptors, k in (1, 2), no
+    masks / crossCheck (the reference uses none)."""
+
+    def __init__(self, normType: int = NORM_L1, crossCheck: bool = False, ctx: Context | None = None):
+        if normType != NORM_L1 or crossCheck:
+            raise ValueError("only BFMatcher(NORM_L1) without crossCheck is implemented")
+        self._ctx = ctx
+
+    def knnMatch(self, queryDescriptors, trainDescriptors, k: int = 2):
+        ctx = self._ctx or _ctx(1, 1)
+        idx, dist = ctx.knnMatch(queryDescriptors, trainDescriptors, k)
+        return [[DMatch(i, int(idx[i, j]), 0, float(dist[i, j])) for j in range(k) if idx[i, j] >= 0]
+                for i in range(len(idx))]
+
+
+def ratio_test(matches, ratio: float = 0.86):
+    """src/main.cpp:28-40: keep m1 where m1.distance <= ratio * m2.distance
+    (a query with fewer than two matches is skipped)."""
+    return [m[0] for m in matches if len(m) >= 2 and m[0].distance <= ratio * m[1].distance]
