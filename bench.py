@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-fast", action="store_true", help="skip the SIFT_FLAG_FAST leg")
+    p.add_argument("--no-match", action="store_true", help="skip the knnMatch leg (SURVEY 8(f) f2)")
     p.add_argument("--profile-json", default=None, help="also write per-stage stats here")
     return p.parse_args()
 
@@ -66,6 +67,48 @@ def cpu_baseline(rows, cols):
             "keypoints_per_s": round(len(kps) / dt, 1), "seconds": round(dt, 3),
             "sample": f"1 synthetic {cols}x{rows} image (seed 0), full SIFT_NCL restated in C "
                       f"(oracle/sift_oracle.c, gcc -O2 -ffp-contract=off), 1 thread, {len(kps)} keypoints"}
+
+
+def match_leg(ctx, a, desc, offs):
+    """src/main.cpp:27 on the batch's own output: knnMatch(k=2) of image 1's
+    descriptors (queries) against image 0's (train), device buffers, W + K
+    launches timed with the context's HIP events (rank 0 only; not in `value`)."""
+    o = [int(x) for x in offs[:3].tolist()]
+    nt, nq = o[1] - o[0], o[2] - o[1]
+    train, query = desc[o[0]:o[1]], desc[o[1]:o[2]]
+    idx = torch.empty((nq, 2), dtype=torch.int32, device="cuda")
+    dst = torch.empty((nq, 2), dtype=torch.float32, device="cuda")
+    ctx.set_flags(siftgpu.SIFT_FLAG_PROFILE)
+
+    def run():
+        ctx.knn_match_device(query.data_ptr(), nq, train.data_ptr(), nt, 2, idx.data_ptr(), dst.data_ptr())
+    for _ in range(a.warmup):
+        run()
+    ctx.sync()
+    ctx.stage_stats(reset=True)
+    for _ in range(a.steps):
+        run()
+    st = ctx.stage_stats(reset=True)["match"]
+    ms = st["ms"] / max(st["launches"], 1)
+    return {"n_query": nq, "n_train": nt, "ms": ms, "flops": st["flops"] / max(st["launches"], 1),
+            "idx": idx, "dist": dst, "query": query, "train": train}
+
+
+def match_cpu_baseline(m, n_sample=64):
+    """oracle/match.py (numpy, this process's BLAS-free float32 ops) on a sample
+    of the leg's queries against the full train set."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import match as M  # the checker / CPU baseline only
+    q = m["query"][:n_sample].cpu().numpy()
+    t = m["train"].cpu().numpy()
+    t0 = time.perf_counter()
+    ridx, rdist = M.knn_match(q, t, 2)
+    dt = time.perf_counter() - t0
+    same = bool((ridx == m["idx"][:n_sample].cpu().numpy()).all() and
+                (rdist.view("u4") == m["dist"][:n_sample].cpu().numpy().view("u4")).all())
+    return {"value": round(len(q) * len(t) / dt / 1e6, 2), "unit": "Mpairs/s", "cores": 1, "kind": "port",
+            "sample": f"{len(q)} queries x {len(t)} train rows (oracle/match.py, numpy float32, normL1_ order)",
+            "gpu_equals_oracle_on_sample": same}
 
 
 def main():
@@ -129,6 +172,7 @@ def main():
 
     dt, stats, kp_total_step = leg(siftgpu.SIFT_FLAG_PROFILE)
     fast = None if a.no_fast else leg(siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
+    match = None if a.no_match or rank != 0 or B < 2 else match_leg(ctx, a, desc, offs)
 
     if rank == 0:
         mpix = world * B * R * C * a.steps / 1e6
@@ -193,6 +237,22 @@ def main():
                 "note": "algorithmic bytes B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes, "
                         "SURVEY.md 8(d)) over the five per-octave launches of one step, / their summed "
                         "HIP-event time; north_star target frac >= 0.6"}
+        if match is not None:
+            pairs = match["n_query"] * match["n_train"]
+            lane_ops = match["flops"] / (match["ms"] * 1e-3) / 1e12 if match["ms"] else 0.0
+            out["match"] = {
+                "metric": "knnMatch(k=2) L1 distance pairs/s, image 1 vs image 0 of the batch",
+                "value": round(pairs / (match["ms"] * 1e-3) / 1e9, 3) if match["ms"] else None,
+                "unit": "Gpairs/s", "ms": round(match["ms"], 4),
+                "n_query": match["n_query"], "n_train": match["n_train"],
+                "roofline": {"bound": "valu", "achieved": round(lane_ops, 2), "peak": FP32_PEAK_TFLOPS / 2,
+                             "unit": "Tlane-op/s", "frac": round(lane_ops / (FP32_PEAK_TFLOPS / 2), 4),
+                             "kernel": "knn_l1_kernel",
+                             "note": "2 VALU lane-ops (v_sub, v_add |x|) per descriptor element per pair; "
+                                     "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"},
+                "note": "SURVEY 8(f) f2 (src/main.cpp:25-27); bit-exact vs oracle/match.py"}
+            if world == 1 and not a.no_cpu_baseline:
+                out["match"]["cpu_baseline"] = match_cpu_baseline(match)
         if world == 1 and not a.no_cpu_baseline:
             cb = cpu_baseline(R, C)
             out["cpu_baseline"] = cb
