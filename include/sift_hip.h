@@ -139,6 +139,21 @@ int sift_find_scale_space_extrema(sift_ctx* ctx, const float* gpyr, const float*
 int sift_calc_descriptors(sift_ctx* ctx, const float* gpyr, int rows, int cols, int n_octaves,
                           const sift_keypoint* kpts, int n, float* desc, int first_octave);
 
+/* ---- image front end ----------------------------------- */
+/* Replaces the conversion half of the application's readImage
+ * (src/main.cpp:79-87): decoded 8-bit BGR bytes (imread's layout) ->
+ * optional INTER_LINEAR resize to out_rows x out_cols (the scene's
+ * Size(960, 960); no resize when the sizes are equal) -> cvtColor
+ * COLOR_RGB2GRAY on those BGR bytes -> CV_32F.  Decoding stays with the
+ * caller.  Host buffers (synchronous), gray is out_rows x out_cols floats: */
+int sift_bgr8_to_gray(sift_ctx* ctx, const uint8_t* bgr, int rows, int cols, size_t row_stride, int out_rows,
+                      int out_cols, float* gray);
+/* Device buffers, a batch of images, enqueued on the context stream (the
+ * output can be the input of sift_detect_compute_batch). Strides in bytes. */
+int sift_bgr8_to_gray_device(sift_ctx* ctx, const uint8_t* d_bgr, int batch, int rows, int cols,
+                             size_t row_stride, size_t img_stride, int out_rows, int out_cols, float* d_gray,
+                             size_t out_row_stride, size_t out_img_stride);
+
 /* ---- matching ------------------------------------------ */
 /* Replaces `BFMatcher(NORM_L1).knnMatch(query, train, matches, k)` of the
  * reference application (src/main.cpp:25-27; the 0.86 ratio test at :28-40

@@ -910,6 +910,52 @@ int sift_knn_match_l1(sift_ctx* c, const float* query, int n_query, const float*
   return SIFT_OK;
 }
 
+// ---- readImage front end, src/main.cpp:79-87 ----
+int sift_bgr8_to_gray_device(sift_ctx* c, const uint8_t* d_bgr, int batch, int rows, int cols, size_t row_stride,
+                             size_t img_stride, int out_rows, int out_cols, float* d_gray, size_t out_row_stride,
+                             size_t out_img_stride) {
+  if (!c) return SIFT_E_INVALID;
+  if (!d_bgr || !d_gray) return fail(c, SIFT_E_INVALID, "null buffer");
+  if (batch < 1 || rows < 1 || cols < 1 || out_rows < 1 || out_cols < 1)
+    return fail(c, SIFT_E_INVALID, "empty image");
+  if (row_stride < (size_t)cols * 3 || (batch > 1 && img_stride < row_stride * rows))
+    return fail(c, SIFT_E_INVALID, "source strides too small");
+  if (out_row_stride % sizeof(float) || out_img_stride % sizeof(float) ||
+      out_row_stride < (size_t)out_cols * sizeof(float) ||
+      (batch > 1 && out_img_stride < out_row_stride * out_rows))
+    return fail(c, SIFT_E_INVALID, "output strides");
+  (void)hipSetDevice(c->device);
+  {
+    StageScope s(c, ST_UPLOAD, 0, (3.0 * rows * cols + 4.0 * out_rows * out_cols) * batch);
+    launch_bgr8_gray(c->stream, d_bgr, (long long)row_stride, (long long)img_stride, rows, cols, d_gray,
+                     (long long)(out_row_stride / sizeof(float)), (long long)(out_img_stride / sizeof(float)),
+                     out_rows, out_cols, batch);
+  }
+  HIP_TRY(c, hipGetLastError());
+  return SIFT_OK;
+}
+
+int sift_bgr8_to_gray(sift_ctx* c, const uint8_t* bgr, int rows, int cols, size_t row_stride, int out_rows,
+                      int out_cols, float* gray) {
+  if (!c) return SIFT_E_INVALID;
+  if (!bgr || !gray) return fail(c, SIFT_E_INVALID, "null buffer");
+  if (rows < 1 || cols < 1 || out_rows < 1 || out_cols < 1) return fail(c, SIFT_E_INVALID, "empty image");
+  if (row_stride < (size_t)cols * 3) return fail(c, SIFT_E_INVALID, "row stride too small");
+  (void)hipSetDevice(c->device);
+  const size_t sb = align256((size_t)rows * row_stride), ob = (size_t)out_rows * out_cols * sizeof(float);
+  int rc = ensure_match(c, sb + ob);  // the matcher's scratch doubles as staging here
+  if (rc) return rc;
+  uint8_t* d_src = static_cast<uint8_t*>(c->d_match);
+  float* d_out = reinterpret_cast<float*>(static_cast<char*>(c->d_match) + sb);
+  HIP_TRY(c, hipMemcpyAsync(d_src, bgr, (size_t)rows * row_stride, hipMemcpyHostToDevice, c->stream));
+  if ((rc = sift_bgr8_to_gray_device(c, d_src, 1, rows, cols, row_stride, 0, out_rows, out_cols, d_out,
+                                     (size_t)out_cols * sizeof(float), 0)))
+    return rc;
+  HIP_TRY(c, hipMemcpyAsync(gray, d_out, ob, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SIFT_OK;
+}
+
 int sift_get_stage_stats(sift_ctx* c, sift_stage_stat* out, int cap, int* n, int reset) {
   if (!c) return SIFT_E_INVALID;
   drain_profile(c);

@@ -183,6 +183,8 @@ void launch_synth(hipStream_t st, float* out, int batch, int rows, int cols, lon
 // kernel widths are not the unrolled 4 / 4, 8, 12, 18.
 size_t fast_coefs_size();
 int fast_coefs_host(float sigma_base, const float* sig, void* out);
+void launch_bgr8_gray(hipStream_t st, const uint8_t* src, long long sstride, long long simg, int srows, int scols,
+                      float* dst, long long dpitch, long long dimg, int drows, int dcols, int batch);
 int knn_splits(int nq, int nt);
 void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int nt, int k, int splits,
                    float2* part_d, int2* part_i, int* idx, float* dist);

@@ -97,6 +97,8 @@ def lib():
             "sift_get_stage_stats": (ip, [vp, ctypes.POINTER(StageStat), ip, pint, ip]),
             "sift_selftest_math": (ip, [vp, ip, fp, fp, fp, ip]),
             "sift_knn_match_l1": (ip, [vp, fp, ip, fp, ip, ip, pint, fp]),
+            "sift_bgr8_to_gray": (ip, [vp, vp, ip, ip, sz, ip, ip, fp]),
+            "sift_bgr8_to_gray_device": (ip, [vp, vp, ip, ip, ip, sz, sz, ip, ip, vp, sz, sz]),
             "sift_knn_match_l1_device": (ip, [vp, vp, ip, vp, ip, ip, vp, vp]),
         }
         for name, (res, args) in sigs.items():
@@ -261,6 +263,27 @@ class Context:
                                                   _fp(desc), firstOctave))
         return desc
 
+    def bgr8_to_gray(self, bgr: np.ndarray, out_rows: int | None = None, out_cols: int | None = None):
+        """readImage's conversion (src/main.cpp:83-85) of decoded BGR bytes:
+        optional INTER_LINEAR resize, COLOR_RGB2GRAY on BGR, CV_32F."""
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        if bgr.ndim != 3 or bgr.shape[2] != 3:
+            raise ValueError("expected an H x W x 3 uint8 BGR image")
+        r, c = bgr.shape[:2]
+        orows, ocols = out_rows or r, out_cols or c
+        gray = np.empty((orows, ocols), np.float32)
+        self._check("sift_bgr8_to_gray",
+                    self._L.sift_bgr8_to_gray(self.h, bgr.ctypes.data, r, c, c * 3, orows, ocols, _fp(gray)))
+        return gray
+
+    def bgr8_to_gray_device(self, src_ptr: int, batch: int, rows: int, cols: int, row_stride: int,
+                            img_stride: int, out_rows: int, out_cols: int, dst_ptr: int, out_row_stride: int,
+                            out_img_stride: int):
+        self._check("sift_bgr8_to_gray_device",
+                    self._L.sift_bgr8_to_gray_device(self.h, ctypes.c_void_p(src_ptr), batch, rows, cols,
+                                                     row_stride, img_stride, out_rows, out_cols,
+                                                     ctypes.c_void_p(dst_ptr), out_row_stride, out_img_stride))
+
     def knnMatch(self, query: np.ndarray, train: np.ndarray, k: int = 2):
         """BFMatcher(NORM_L1).knnMatch as arrays (src/main.cpp:25-27): idx, dist
         [n_query, k]; idx -1 / dist +inf where there are fewer than k train rows."""
@@ -354,6 +377,26 @@ def findScaleSpaceExtrema(gpyr, dogpyr, nOctaves=5):
 
 def calDescriptor(gpyr, keypoints, firstOctave=0):
     return _ctx(*gpyr[0].shape).calDescriptor(gpyr, keypoints, firstOctave)
+
+
+# ---- image front end -------------------------------------
+def imread(filename) -> np.ndarray:
+    """cv::imread(filename) layout: H x W x 3 uint8 BGR (decoded with PIL)."""
+    from PIL import Image
+    rgb = np.asarray(Image.open(filename).convert("RGB"), np.uint8)
+    return np.ascontiguousarray(rgb[..., ::-1])
+
+
+def readImage(filename_or_bgr, resized: bool):
+    """src/main.cpp:79-87 -> (img, gray): gray is the CV_32F plane SIFT_NCL
+    takes (960 x 960 when resized), produced on the GPU (frontend.hip); img is
+    the decoded BGR image (the reference keeps the resized copy, which only its
+    drawMatches uses -- not produced here)."""
+    bgr = imread(filename_or_bgr) if isinstance(filename_or_bgr, (str, os.PathLike)) else \
+        np.ascontiguousarray(filename_or_bgr, np.uint8)
+    rows, cols = (960, 960) if resized else bgr.shape[:2]
+    gray = _ctx(rows, cols).bgr8_to_gray(bgr, rows, cols)
+    return bgr, gray
 
 
 # ---- matcher (SURVEY.md 8(f) f2): the reference application's consumer ------
