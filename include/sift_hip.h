@@ -169,6 +169,17 @@ int sift_knn_match_l1(sift_ctx* ctx, const float* query, int n_query, const floa
 int sift_knn_match_l1_device(sift_ctx* ctx, const float* d_query, int n_query, const float* d_train,
                              int n_train, int k, int* d_idx, float* d_dist);
 
+/* ---- homography ---------------------------------------- */
+/* Replaces `findHomography(obj, scene, RANSAC)` and `perspectiveTransform`
+ * (src/main.cpp:54-62): n point pairs as interleaved (x, y) floats, OpenCV's
+ * defaults are ransac_thresh 3, max_iters 2000, confidence 0.995.  H is a
+ * row-major 3x3 with H[8] = 1; inlier_mask (n bytes, may be NULL) gets the
+ * RANSAC inliers.  Host code, no context.  SIFT_E_INVALID (H zeroed) when no
+ * model is found or n < 4 -- OpenCV's empty Mat. */
+int sift_find_homography(const float* src_xy, const float* dst_xy, int n, double ransac_thresh, int max_iters,
+                         double confidence, double* H, unsigned char* inlier_mask);
+int sift_perspective_transform(const double* H, const float* xy, int n, float* out_xy);
+
 /* ---- self-test ------------------------------------------------------------ */
 /* Evaluates one device arithmetic helper element-wise on host arrays (n
  * values), for bit-exact checks of the GPU math against the CPU oracle:

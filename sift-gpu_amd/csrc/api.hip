@@ -956,6 +956,23 @@ int sift_bgr8_to_gray(sift_ctx* c, const uint8_t* bgr, int rows, int cols, size_
   return SIFT_OK;
 }
 
+// ---- findHomography(RANSAC) + perspectiveTransform, src/main.cpp:54-62 ----
+int sift_find_homography(const float* src_xy, const float* dst_xy, int n, double ransac_thresh, int max_iters,
+                         double confidence, double* H, unsigned char* inlier_mask) {
+  if (!src_xy || !dst_xy || !H || n < 0) return SIFT_E_INVALID;
+  if (!find_homography_ransac(src_xy, dst_xy, n, ransac_thresh, max_iters, confidence, H, inlier_mask)) {
+    for (int i = 0; i < 9; ++i) H[i] = 0;  // OpenCV returns an empty Mat
+    return SIFT_E_INVALID;
+  }
+  return SIFT_OK;
+}
+
+int sift_perspective_transform(const double* H, const float* xy, int n, float* out_xy) {
+  if (!H || n < 0 || (n > 0 && (!xy || !out_xy))) return SIFT_E_INVALID;
+  perspective_transform(H, xy, n, out_xy);
+  return SIFT_OK;
+}
+
 int sift_get_stage_stats(sift_ctx* c, sift_stage_stat* out, int cap, int* n, int reset) {
   if (!c) return SIFT_E_INVALID;
   drain_profile(c);

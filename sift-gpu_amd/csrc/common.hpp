@@ -185,6 +185,9 @@ size_t fast_coefs_size();
 int fast_coefs_host(float sigma_base, const float* sig, void* out);
 void launch_bgr8_gray(hipStream_t st, const uint8_t* src, long long sstride, long long simg, int srows, int scols,
                       float* dst, long long dpitch, long long dimg, int drows, int dcols, int batch);
+int find_homography_ransac(const float* src_xy, const float* dst_xy, int n, double thr, int max_iters,
+                           double confidence, double* H, unsigned char* mask_out);
+void perspective_transform(const double* H, const float* xy, int n, float* out);
 int knn_splits(int nq, int nt);
 void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int nt, int k, int splits,
                    float2* part_d, int2* part_i, int* idx, float* dist);

@@ -98,6 +98,9 @@ def lib():
             "sift_selftest_math": (ip, [vp, ip, fp, fp, fp, ip]),
             "sift_knn_match_l1": (ip, [vp, fp, ip, fp, ip, ip, pint, fp]),
             "sift_bgr8_to_gray": (ip, [vp, vp, ip, ip, sz, ip, ip, fp]),
+            "sift_find_homography": (ip, [fp, fp, ip, ctypes.c_double, ip, ctypes.c_double,
+                                          ctypes.POINTER(ctypes.c_double), vp]),
+            "sift_perspective_transform": (ip, [ctypes.POINTER(ctypes.c_double), fp, ip, fp]),
             "sift_bgr8_to_gray_device": (ip, [vp, vp, ip, ip, ip, sz, sz, ip, ip, vp, sz, sz]),
             "sift_knn_match_l1_device": (ip, [vp, vp, ip, vp, ip, ip, vp, vp]),
         }
@@ -436,3 +439,39 @@ def ratio_test(matches, ratio: float = 0.86):
     """src/main.cpp:28-40: keep m1 where m1.distance <= ratio * m2.distance
     (a query with fewer than two matches is skipped)."""
     return [m[0] for m in matches if len(m) >= 2 and m[0].distance <= ratio * m[1].distance]
+
+
+# ---- homography (SURVEY.md 8(f) f4): src/main.cpp:44-62 ------------------------
+RANSAC = 8  # cv::RANSAC
+
+
+def findHomography(srcPoints, dstPoints, method: int = RANSAC, ransacReprojThreshold: float = 3.0,
+                   mask=None, maxIters: int = 2000, confidence: float = 0.995):
+    """cv::findHomography(obj, scene, RANSAC) -> (H 3x3 float64 or None, inlier mask).
+    Host code in the library (homography.hip); None where OpenCV returns an empty Mat."""
+    if method != RANSAC:
+        raise ValueError("only RANSAC is implemented (the reference uses RANSAC)")
+    src = np.ascontiguousarray(srcPoints, np.float32).reshape(-1, 2)
+    dst = np.ascontiguousarray(dstPoints, np.float32).reshape(-1, 2)
+    if len(src) != len(dst):
+        raise ValueError("point counts differ")
+    H = np.zeros(9, np.float64)
+    m = np.zeros(max(len(src), 1), np.uint8)
+    rc = lib().sift_find_homography(_fp(src), _fp(dst), len(src), float(ransacReprojThreshold), int(maxIters),
+                                    float(confidence), H.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                    m.ctypes.data)
+    if rc != SIFT_OK:
+        return None, np.zeros(len(src), np.uint8)
+    return H.reshape(3, 3), m[:len(src)]
+
+
+def perspectiveTransform(points, H):
+    """cv::perspectiveTransform for Point2f with a 3x3 double H."""
+    pts = np.ascontiguousarray(points, np.float32).reshape(-1, 2)
+    Hd = np.ascontiguousarray(H, np.float64).reshape(9)
+    out = np.empty_like(pts)
+    rc = lib().sift_perspective_transform(Hd.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), _fp(pts), len(pts),
+                                          _fp(out))
+    if rc != SIFT_OK:
+        raise SiftError("sift_perspective_transform", rc, "bad argument")
+    return out
