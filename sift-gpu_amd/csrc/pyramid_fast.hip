@@ -421,43 +421,44 @@ __device__ __forceinline__ void hb_pass(const float4* __restrict__ stage4, float
   hb4[((Y + 2 * s + 1) & (kHbRows - 1)) * (kBP / 4) + j] = make_float4(acc[0].y, acc[1].y, acc[2].y, acc[3].y);
 }
 
-// Octave-0 column pass of the base blur for base rows [Z, Z+8) and base
-// columns (2p, 2p+1), from row-pass ring rows [Z-4, Z+12) starting at slot
-// S0 = (Z - 4) & 15.  Writes the plane-0 interior to HBM and the padded copy
+// Octave-0 column pass of the base blur for base rows [Z+H, Z+H+4) and base
+// columns (2p, 2p+1), from row-pass ring rows [Z+H-4, Z+H+8) starting at slot
+// S0 = (Z + H - 4) & 15.  Both wave roles take a half (H = 0: waves 0-1,
+// H = 4: waves 2-3), so the phase is 36 packed FMAs deep, not 72.  Writes the plane-0 interior to HBM and the padded copy
 // (0 outside [0, rows-1) x [0, cols-1)) into the row-pair interleaved base
 // rows.  c = 2p is even, so a pair is entirely inside or outside the strip's
 // output columns.
-template <int S0>
+template <int S0, int H>
 __device__ __forceinline__ void base_col(const FastArgs& A, const f2* g, const float* __restrict__ hb,
                                          float4* __restrict__ bs4, Rsrc rs0, int p, int Z, int x0, int y0,
                                          int y1) {
   LdsF2 h2[4];  // see lds_bases (hb rows are 688 B apart)
   lds_bases(reinterpret_cast<const f2*>(hb) + p, h2);
-  f2 win[16];
+  f2 win[12];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) win[k] = h2[k & 3][((S0 + k) & (kHbRows - 1)) * (kBP / 2)];
-  f2 acc[8];
+  for (int k = 0; k < 12; ++k) win[k] = h2[k & 3][((S0 + k) & (kHbRows - 1)) * (kBP / 2)];
+  f2 acc[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = splat(0.f);
+  for (int i = 0; i < 4; ++i) acc[i] = splat(0.f);
 #pragma unroll
   for (int a = 0; a < 9; ++a) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = pk_tap(win[i + a], g, a, acc[i]);
+    for (int i = 0; i < 4; ++i) acc[i] = pk_tap(win[i + a], g, a, acc[i]);
   }
   const int c = 2 * p, x = x0 - kH + c;
   const bool colout = c >= kH && c < kH + kFW && x < A.cols;
   const bool oka = x >= 0 && x < A.cols - 1, okb = x + 1 >= 0 && x + 1 < A.cols - 1;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = H / 2; s < H / 2 + 2; ++s) {
     const int y = Z + 2 * s;
-    const f2 e0 = acc[2 * s], e1 = acc[2 * s + 1];
+    const f2 e0 = acc[2 * s - H], e1 = acc[2 * s + 1 - H];
     st_plane2(rs0, (colout && y >= y0 && y < y1) ? (y * A.pitch + x) * 4 : kDrop, e0);
     st_plane2(rs0, (colout && y + 1 >= y0 && y + 1 < y1) ? ((y + 1) * A.pitch + x) * 4 : kDrop, e1);
     const bool ok0 = y >= 0 && y < A.rows - 1, ok1 = y + 1 >= 0 && y + 1 < A.rows - 1;
     bs4[s * (kBP2 / 4) + p] = make_float4((ok0 && oka) ? e0.x : 0.f, (ok1 && oka) ? e1.x : 0.f,
                                           (ok0 && okb) ? e0.y : 0.f, (ok1 && okb) ? e1.y : 0.f);
   }
-  asm volatile("; base_col %0" ::"n"(S0));  // see col_fixed
+  asm volatile("; base_col %0 %1" ::"n"(S0), "n"(H));  // see col_fixed
 }
 
 // LDS carve-up and per-workgroup constants of the step walk.
@@ -507,12 +508,13 @@ __device__ __forceinline__ void walk(const FastArgs& A, const Walk& K, int wv) {
     if (OCT0) {
       hb_pass(K.stage4, K.hb4, kb, Z + 4);
       __syncthreads();
-      if (t < kBW / 2) {
+      constexpr int H = WA == 18 ? 0 : 4;  // this role's half of the base rows
+      if ((t & 127) < kBW / 2) {
         const float* hb = reinterpret_cast<const float*>(K.hb4);
         if (Z & 8)
-          base_col<4>(A, kb, hb, K.stage4, K.rs0, t, Z, x0, y0, y1);
+          base_col<(4 + H) & 15, H>(A, kb, hb, K.stage4, K.rs0, t & 127, Z, x0, y0, y1);
         else
-          base_col<12>(A, kb, hb, K.stage4, K.rs0, t, Z, x0, y0, y1);
+          base_col<(12 + H) & 15, H>(A, kb, hb, K.stage4, K.rs0, t & 127, Z, x0, y0, y1);
       }
       __syncthreads();
     }
