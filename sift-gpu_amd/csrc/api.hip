@@ -283,8 +283,9 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
   }
 }
 
-// dog_from_gpyr: the fused extrema pass also forms (and writes) the DoG planes
-// from the Gaussian pyramid; otherwise the DoG planes are already resident
+// dog_from_gpyr: the fused extrema pass forms the DoG values from the Gaussian
+// pyramid and refinement re-forms the few it needs, so no DoG plane is written
+// (SIFT_NCL never returns them); otherwise the DoG planes are already resident
 // (sift_find_scale_space_extrema uploads both pyramids).
 void enqueue_detect(sift_ctx* c, const Layout& L, int batch, sift_keypoint* kpts, int kp_cap,
                     int* img_off, bool dog_from_gpyr) {
@@ -295,7 +296,7 @@ void enqueue_detect(sift_ctx* c, const Layout& L, int batch, sift_keypoint* kpts
   }
   {
     StageScope s(c, ST_REFINE);
-    launch_refine_orient(st, L, c->d_gpyr, c->d_grad, c->d_dog, c->d_mc, c->D, batch);
+    launch_refine_orient(st, L, c->d_gpyr, c->d_grad, dog_from_gpyr ? nullptr : c->d_dog, c->d_mc, c->D, batch);
   }
   {
     StageScope s(c, ST_EMIT);

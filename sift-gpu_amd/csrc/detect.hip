@@ -88,7 +88,7 @@ struct TileArgs {
   unsigned* mask;
   int tile_start[kMaxOctaves + 1];
   int tiles_x[kMaxOctaves];
-  int write_dog;  // 1: form DoG from the Gaussian planes and write it; 0: read the DoG planes
+  int write_dog;  // 1: form DoG from the Gaussian planes (not stored); 0: read the DoG planes
 };
 
 // src/sift.cpp:493-511 on an LDS tile: v at (y, x) of plane cur; ties pass.
@@ -144,16 +144,12 @@ __global__ __launch_bounds__(256) void dog_extrema_kernel(TileArgs A) {
       g2 = g[O.g_off[2] + p];
       if (A.write_dog) {
         const float g0 = g[O.g_off[0] + p], g3 = g[O.g_off[3] + p], g4 = g[O.g_off[4] + p];
+        // Not stored: refinement forms the same differences from the Gaussian
+        // planes (refine_candidate<true>), which saves 16 B/px of HBM writes.
         d0 = g1 - g0;
         d1 = g2 - g1;
         d2 = g3 - g2;
         d3 = g4 - g3;
-        if (rr >= 1 && rr <= kExTH && cc >= 1 && cc <= kExTW) {
-          dg[O.d_off[0] + p] = d0;
-          dg[O.d_off[1] + p] = d1;
-          dg[O.d_off[2] + p] = d2;
-          dg[O.d_off[3] + p] = d3;
-        }
       } else {
         d0 = dg[O.d_off[0] + p];
         d1 = dg[O.d_off[1] + p];
@@ -402,6 +398,7 @@ struct RefArgs {
   const float* gpyr;
   const float2* grad;
   const float* dog;
+  int dog_from_g;  // 1: DoG values are Gaussian-plane differences (no DoG planes stored)
   const MathConsts* mc;
   const Cand* cands;
   const int* cand_total;
@@ -418,8 +415,13 @@ struct Refined {
   float x, y, size, response;
 };
 
+// DoG value of layer l at (yy, xx): the stored DoG plane, or -- FROM_G -- the
+// difference of the Gaussian planes l+1 and l that buildDoGPyramid stores
+// (src/sift.cpp:276; the same float subtraction, so bit-identical).
+template <bool FROM_G>
 __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const float* __restrict__ dimg,
-                                                    int o, int layer, int r, int c) {
+                                                    const float* __restrict__ gimg, int o, int layer, int r,
+                                                    int c) {
   const Octave& O = Lay.oct[o];
   const long long pitch = O.pitch;
   const float img_scale = 1. / 255;
@@ -430,11 +432,14 @@ __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const flo
   Refined R{};
   R.ok = true;
   int it = 0;
-#define AT(pl, yy, xx) ((pl)[(long long)(yy)*pitch + (xx)])
+  auto D = [&](int l, int yy, int xx) -> float {
+    const long long p = (long long)yy * pitch + xx;
+    if (FROM_G) return gimg[O.g_off[l + 1] + p] - gimg[O.g_off[l] + p];
+    return dimg[O.d_off[l] + p];
+  };
+#define AT(pl, yy, xx) D(pl, yy, xx)
   for (; it < kMaxInterp; ++it) {
-    const float* cur = dimg + O.d_off[layer];
-    const float* lo = dimg + O.d_off[layer - 1];
-    const float* hi = dimg + O.d_off[layer + 1];
+    const int cur = layer, lo = layer - 1, hi = layer + 1;
     const float g[3] = {(AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale,
                         (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale,
                         (AT(hi, r, c) - AT(lo, r, c)) * deriv_scale};
@@ -474,9 +479,7 @@ __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const flo
     return R;
   }
   {
-    const float* cur = dimg + O.d_off[layer];
-    const float* lo = dimg + O.d_off[layer - 1];
-    const float* hi = dimg + O.d_off[layer + 1];
+    const int cur = layer, lo = layer - 1, hi = layer + 1;
     const float g0 = (AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale;
     const float g1 = (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale;
     const float g2 = (AT(hi, r, c) - AT(lo, r, c)) * deriv_scale;
@@ -546,7 +549,10 @@ __global__ __launch_bounds__(64) void refine_orient_kernel(RefArgs A) {
     Cand cd{0, 0, 0, 0};
     if (ci < cend) {
       cd = A.cands[ci];
-      R = refine_candidate(A.L, A.dog + cd.b * A.L.d_img, cd.ol & 255, cd.ol >> 8, cd.r, cd.c);
+      R = A.dog_from_g ? refine_candidate<true>(A.L, nullptr, A.gpyr + cd.b * A.L.g_img, cd.ol & 255, cd.ol >> 8,
+                                                cd.r, cd.c)
+                       : refine_candidate<false>(A.L, A.dog + cd.b * A.L.d_img, nullptr, cd.ol & 255,
+                                                 cd.ol >> 8, cd.r, cd.c);
     }
     const int o = cd.ol & 255;
     const Octave& O = A.L.oct[o];
@@ -659,6 +665,7 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.gpyr = gpyr;
   A.grad = grad;
   A.dog = dog;
+  A.dog_from_g = dog == nullptr;
   A.mc = mc;
   A.cands = D.cands;
   A.cand_total = D.cand_total;
