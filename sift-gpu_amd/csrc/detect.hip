@@ -134,35 +134,60 @@ __global__ __launch_bounds__(256) void dog_extrema_kernel(TileArgs A) {
   float* dg = A.dog + b * A.L.d_img;
   // DoG tile with a one-pixel halo, computed from the five Gaussian planes
   // (or read, when the caller supplied the DoG pyramid)
-  for (int i = threadIdx.x; i < (kExTH + 2) * (kExTW + 2); i += 256) {
+  // Branch-free (clamped addresses, then a select): all 5 items of a lane
+  // have their loads in flight together instead of one HBM round trip each.
+  constexpr int kN = (kExTH + 2) * (kExTW + 2), kIt = (kN + 255) / 256;
+  float ld[kIt][6];
+  bool okv[kIt];
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int i = min((int)threadIdx.x + 256 * u, kN - 1);
     const int rr = i / (kExTW + 2), cc = i % (kExTW + 2);
     const int y = y0 - 1 + rr, x = x0 - 1 + cc;
-    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f, g1 = 0.f, g2 = 0.f;
-    if (y >= 0 && y < O.rows && x >= 0 && x < O.cols) {
-      const long long p = (long long)y * pitch + x;
-      g1 = g[O.g_off[1] + p];
-      g2 = g[O.g_off[2] + p];
+    okv[u] = y >= 0 && y < O.rows && x >= 0 && x < O.cols;
+    const long long p = (long long)min(max(y, 0), O.rows - 1) * pitch + min(max(x, 0), O.cols - 1);
+    ld[u][0] = g[O.g_off[1] + p];
+    ld[u][1] = g[O.g_off[2] + p];
+    if (A.write_dog) {
+      ld[u][2] = g[O.g_off[0] + p];
+      ld[u][3] = g[O.g_off[3] + p];
+      ld[u][4] = g[O.g_off[4] + p];
+      ld[u][5] = 0.f;
+    } else {
+      ld[u][2] = dg[O.d_off[0] + p];
+      ld[u][3] = dg[O.d_off[1] + p];
+      ld[u][4] = dg[O.d_off[2] + p];
+      ld[u][5] = dg[O.d_off[3] + p];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i < kN) {
+      const int rr = i / (kExTW + 2), cc = i % (kExTW + 2);
+      const float g1 = okv[u] ? ld[u][0] : 0.f, g2 = okv[u] ? ld[u][1] : 0.f;
+      float d0, d1, d2, d3;
       if (A.write_dog) {
-        const float g0 = g[O.g_off[0] + p], g3 = g[O.g_off[3] + p], g4 = g[O.g_off[4] + p];
         // Not stored: refinement forms the same differences from the Gaussian
         // planes (refine_candidate<true>), which saves 16 B/px of HBM writes.
+        const float g0 = okv[u] ? ld[u][2] : 0.f, g3 = okv[u] ? ld[u][3] : 0.f, g4 = okv[u] ? ld[u][4] : 0.f;
         d0 = g1 - g0;
         d1 = g2 - g1;
         d2 = g3 - g2;
         d3 = g4 - g3;
       } else {
-        d0 = dg[O.d_off[0] + p];
-        d1 = dg[O.d_off[1] + p];
-        d2 = dg[O.d_off[2] + p];
-        d3 = dg[O.d_off[3] + p];
+        d0 = okv[u] ? ld[u][2] : 0.f;
+        d1 = okv[u] ? ld[u][3] : 0.f;
+        d2 = okv[u] ? ld[u][4] : 0.f;
+        d3 = okv[u] ? ld[u][5] : 0.f;
       }
+      sd[0][rr][cc] = d0;
+      sd[1][rr][cc] = d1;
+      sd[2][rr][cc] = d2;
+      sd[3][rr][cc] = d3;
+      sg[0][rr][cc] = g1;
+      sg[1][rr][cc] = g2;
     }
-    sd[0][rr][cc] = d0;
-    sd[1][rr][cc] = d1;
-    sd[2][rr][cc] = d2;
-    sd[3][rr][cc] = d3;
-    sg[0][rr][cc] = g1;
-    sg[1][rr][cc] = g2;
   }
   __syncthreads();
   // Per-pixel gradient of layers 1 and 2 -- the (magnitude, orientation) that
