@@ -136,6 +136,24 @@ def test_sift_ncl_1080p_golden(ctx, oracle):
     assert np.all(np.diff(kps["octave"] & 255) >= 0)
 
 
+def test_sift_ncl_8k_golden(siftgpu, oracle):
+    """Maximum size: a 7680x4320 image (16x the 1080p workload) against the
+    oracle's digests (tests/golden/make_golden.py --8k): every Gaussian and DoG
+    plane, the 214,633 keypoints and their descriptors, bit for bit."""
+    g = load_golden("synth0_4320x7680")
+    img = oracle.synth_image(0, 4320, 7680)
+    with siftgpu.Context(4320, 7680, 1, device=0) as c8k:
+        gp = c8k.buildGaussianPyramid(img, 5)
+        assert [sha(p) for p in gp] == list(g["gpyr_sha"])
+        dp = c8k.buildDoGPyramid(gp, 5)
+        assert [sha(p) for p in dp] == list(g["dog_sha"])
+        del gp, dp
+        kps, desc = c8k.SIFT_NCL(img)
+    assert len(kps) == int(g["n"]) == 214633
+    assert sha(kps) == str(g["kp_sha"])
+    assert sha(desc) == str(g["desc_sha"])
+
+
 def test_plateaus_and_ties(ctx, oracle):
     """Blocky input: many exactly-equal DoG neighbours exercise the >= ties."""
     rng = np.random.default_rng(4)
