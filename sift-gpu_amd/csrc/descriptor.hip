@@ -33,6 +33,7 @@ __device__ __forceinline__ void wave_sync_d() {
 }
 
 constexpr int kGrp = 8;            // keypoints per wave
+constexpr int kChunk = 64;         // keypoints ranked together by window radius
 constexpr int kQBins = 45;         // bins per parity class: 3 x 3 x 5
 constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
 constexpr int kRecStride2 = 132;   // words per sample row of the owner records (128 + pad)
@@ -75,6 +76,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   __shared__ int rows_tab[kGrp][kMaxWinRows];       // per row: (jlo + 64) | len << 16
   __shared__ float bc[kGrp][4];
   __shared__ float etab[64];
+  __shared__ int sord[kGrp];                        // this sub-batch's keypoint indices
   const int lane = threadIdx.x & 63;
   const int g = lane >> 3, q = lane & 7;
   const int d = kDescW, nb = kDescBins;
@@ -87,10 +89,39 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   // one contiguous eighth of the raster-ordered keypoints and its L2 sees the
   // overlapping windows of neighbouring keypoints.
   const int xcd = blockIdx.x & 7, nslot = gridDim.x >> 3, slot = blockIdx.x >> 3;
-  const int per = ((n + 7) / 8 + kGrp - 1) / kGrp * kGrp;
+  //
+  // Lane balance (speed only): a wave's sample loop runs to the largest window
+  // of its 8 keypoints, and consecutive keypoints differ in window radius (layer,
+  // sub-layer offset), so each chunk of 64 consecutive keypoints is ranked by
+  // radius and each sub-batch of the chunk takes 8 consecutive ranks.  Keypoints are
+  // independent; only the processing order changes.
+  const int per = ((n + 7) / 8 + kChunk - 1) / kChunk * kChunk;
+  const int k0 = xcd * per;
   const int kend = min(n, (xcd + 1) * per);
-  for (int kb = xcd * per + slot * kGrp; kb < kend; kb += nslot * kGrp) {
-    const int k = kb + g;
+  // whole chunks: a sub-batch past kend may still draw valid ranks
+  const int cend = k0 + (max(kend - k0, 0) + kChunk - 1) / kChunk * kChunk;
+  for (int kb = k0 + slot * kGrp; kb < cend; kb += nslot * kGrp) {
+    // slot s walks sub-batches s, s + nslot, ...; the XOR with the pass index
+    // cycles its windows so no wave always draws the largest ranks
+    const int rel8 = (kb - k0) / kGrp, pass = rel8 / nslot;
+    const int kc = k0 + (rel8 / 8) * kChunk, win = (((rel8 & 7) ^ (pass & 7))) * kGrp;
+    {
+      const int kk = kc + lane;
+      int key = 0x1ffffff;  // past the end: ranked last
+      if (kk < kend) {
+        int oc = A.kpts[kk].octave & 255;
+        oc = oc < 128 ? oc : (-128 | oc);
+        const float sc = oc >= 0 ? 1.f / (1 << (oc & 31)) : (float)(1 << ((-oc) & 31));
+        key = min(max(cv_round(A.kpts[kk].size * sc * 1.5f * 1.4142135623730951f * (d + 1) * 0.5f), 0), 0xffffff);
+      }
+      key = (key << 6) | lane;
+      int rank = 0;
+#pragma unroll
+      for (int m = 0; m < 64; ++m) rank += __builtin_amdgcn_readlane(key, m) < key ? 1 : 0;
+      if (rank >= win && rank < win + kGrp) sord[rank - win] = kk;
+      wave_sync_d();
+    }
+    const int k = sord[g];
     bool active = k < kend;
     int b = 0, oi = 0, layer = 0;
     sift_keypoint kp{};
