@@ -63,9 +63,9 @@ struct Cand {            // one 26-neighbour extremum, in reference scan order
 
 struct CandOut {         // result of refine + orientation for one candidate
   float x, y, size, response;
-  int octave, npeaks, img, pad_;
+  int octave, npeaks, img, ref_r;  // npeaks: 1 if refinement kept it (the count is in DetectBufs::npeaks)
   float angle[kMaxPeaks];
-  float pad2_[2];
+  int ref_c, ref_layer;            // refined integer position / layer (orientation input)
 };
 
 // ---- OpenCV scalar helpers --------------------------

@@ -432,8 +432,7 @@ struct RefArgs {
   int* npeaks;
 };
 
-// adjustLocalExtrema (src/sift.cpp:287-388) for one candidate; every lane of
-// a group evaluates it redundantly (uniform control, broadcast loads).
+// adjustLocalExtrema (src/sift.cpp:287-388) for one candidate.
 struct Refined {
   bool ok;
   int layer, r, c, octave;
@@ -542,19 +541,54 @@ __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const flo
   return R;
 }
 
-// Eight candidates per wave (lanes 8g..8g+7 own candidate g).  Orientation
-// samples are computed 8 at a time per group and added to the group's 36-bin
-// histogram in raster order, lane q of the group at step q (ds_add_f32; one
-// instruction advances all eight groups' ordered chains).
+// Refinement: one lane per candidate.  Writes the refined keypoint fields and
+// the orientation pass's inputs (refined r, c, layer; npeaks = 1 if kept).
+__global__ __launch_bounds__(256) void refine_kernel(RefArgs A) {
+  int n = *A.cand_total;
+  if (n > A.cand_cap) n = A.cand_cap;
+  for (int ci = blockIdx.x * 256 + threadIdx.x; ci < n; ci += gridDim.x * 256) {
+    const Cand cd = A.cands[ci];
+    const Refined R = A.dog_from_g ? refine_candidate<true>(A.L, nullptr, A.gpyr + cd.b * A.L.g_img, cd.ol & 255,
+                                                            cd.ol >> 8, cd.r, cd.c)
+                                   : refine_candidate<false>(A.L, A.dog + cd.b * A.L.d_img, nullptr, cd.ol & 255,
+                                                             cd.ol >> 8, cd.r, cd.c);
+    CandOut* co = A.couts + ci;
+    co->x = R.x;
+    co->y = R.y;
+    co->size = R.size;
+    co->response = R.response;
+    co->octave = R.octave;
+    co->img = cd.b;
+    co->npeaks = R.ok ? 1 : 0;
+    co->ref_r = R.r;
+    co->ref_c = R.c;
+    co->ref_layer = R.layer;
+  }
+}
+
+// Orientation histograms: eight candidates per wave (lanes 8g..8g+7 own
+// candidate g).  Samples are computed 8 at a time per group and added to the
+// group's 36-bin histogram in raster order, lane q of the group at step q
+// (ds_add_f32; one instruction advances all eight groups' ordered chains).
+// Lane balance (speed only): each chunk of 64 consecutive candidates is ranked
+// by window radius (rejected candidates first, radius 0) and each sub-batch
+// takes 8 consecutive ranks, as in descriptor.hip.
 constexpr int kOGrp = 8;
+constexpr int kOChunk = 64;
 
 __device__ __forceinline__ void ohist_add(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-__global__ __launch_bounds__(64) void refine_orient_kernel(RefArgs A) {
+__device__ __forceinline__ int ori_radius(float size, int o) {
+  const float scl = size * 0.5f / (1 << o);
+  return cv_round(3 * 1.5f * scl);
+}
+
+__global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
   __shared__ float oh[kOGrp][kOriBins + 4];
   __shared__ float sm[kOGrp][kOriBins + 4];
+  __shared__ int sord[kOGrp];
   const int lane = threadIdx.x & 63;
   const int g = lane >> 3, q = lane & 7;
   int n = *A.cand_total;
@@ -566,30 +600,51 @@ __global__ __launch_bounds__(64) void refine_orient_kernel(RefArgs A) {
 
   // XCD-aware contiguous split of the raster-ordered candidates (speed only)
   const int xcd = blockIdx.x & 7, nslot = gridDim.x >> 3, slot = blockIdx.x >> 3;
-  const int per = ((n + 7) / 8 + kOGrp - 1) / kOGrp * kOGrp;
+  const int per = ((n + 7) / 8 + kOChunk - 1) / kOChunk * kOChunk;
+  const int c0 = xcd * per;
   const int cend = min(n, (xcd + 1) * per);
-  for (int cb = xcd * per + slot * kOGrp; cb < cend; cb += nslot * kOGrp) {
-    const int ci = cb + g;
-    Refined R{};
-    Cand cd{0, 0, 0, 0};
-    if (ci < cend) {
-      cd = A.cands[ci];
-      R = A.dog_from_g ? refine_candidate<true>(A.L, nullptr, A.gpyr + cd.b * A.L.g_img, cd.ol & 255, cd.ol >> 8,
-                                                cd.r, cd.c)
-                       : refine_candidate<false>(A.L, A.dog + cd.b * A.L.d_img, nullptr, cd.ol & 255,
-                                                 cd.ol >> 8, cd.r, cd.c);
+  const int chend = c0 + (max(cend - c0, 0) + kOChunk - 1) / kOChunk * kOChunk;
+  for (int cb = c0 + slot * kOGrp; cb < chend; cb += nslot * kOGrp) {
+    const int rel8 = (cb - c0) / kOGrp, pass = rel8 / nslot;
+    const int kc = c0 + (rel8 / 8) * kOChunk, win = ((rel8 & 7) ^ (pass & 7)) * kOGrp;
+    {
+      const int kk = kc + lane;
+      int key = 0x1ffffff;  // past the end: ranked last
+      if (kk < cend) {
+        const CandOut& co = A.couts[kk];
+        key = co.npeaks ? min(max(ori_radius(co.size, A.cands[kk].ol & 255), 0), 0xffffff) : 0;
+      }
+      key = (key << 6) | lane;
+      int rank = 0;
+#pragma unroll
+      for (int m = 0; m < 64; ++m) rank += __builtin_amdgcn_readlane(key, m) < key ? 1 : 0;
+      if (rank >= win && rank < win + kOGrp) sord[rank - win] = kk;
+      wave_sync();
     }
-    const int o = cd.ol & 255;
+    const int ci = sord[g];
+    bool ok = false;
+    int o = 0, rr = 0, rc = 0, rl = 0, b = 0;
+    float size = 0.f;
+    if (ci < cend) {
+      const CandOut& co = A.couts[ci];
+      ok = co.npeaks != 0;
+      o = A.cands[ci].ol & 255;
+      size = co.size;
+      rr = co.ref_r;
+      rc = co.ref_c;
+      rl = co.ref_layer;
+      b = co.img;
+    }
     const Octave& O = A.L.oct[o];
     const long long pitch = O.pitch;
     // ---- calcOrientationHist, src/sift.cpp:389-458 ----
-    const float scl = R.size * 0.5f / (1 << o);
-    const int radius = R.ok ? cv_round(3 * 1.5f * scl) : 0;
+    const float scl = size * 0.5f / (1 << o);
+    const int radius = ok ? cv_round(3 * 1.5f * scl) : 0;
     const float sigma = 1.5f * scl;
     const float escale = -1.f / (2.f * sigma * sigma);
-    const float2* gimg = A.grad + cd.b * A.L.g_img + O.g_off[R.ok ? R.layer : 0];
+    const float2* gimg = A.grad + b * A.L.g_img + O.g_off[ok ? rl : 0];
     const int D = 2 * radius + 1;
-    const int ns = R.ok ? D * D : 0;
+    const int ns = ok ? D * D : 0;
     for (int t = q; t < kOriBins; t += 8) oh[g][t] = 0.f;
     int nmax = ns;
     nmax = max(nmax, __shfl_xor(nmax, 8));
@@ -602,7 +657,7 @@ __global__ __launch_bounds__(64) void refine_orient_kernel(RefArgs A) {
       float val = 0.f;
       if (s < ns) {
         const int i = s / D - radius, j = s % D - radius;
-        const int y = R.r + i, x = R.c + j;
+        const int y = rr + i, x = rc + j;
         if (!(y <= 0 || y >= O.rows - 1) && !(x <= 0 || x >= O.cols - 1)) {
           const float2 mo = gimg[(long long)y * pitch + x];  // (Mag, Ori) of the pixel
           const float w = exp32f((i * i + j * j) * escale, etab, ek);
@@ -641,7 +696,7 @@ __global__ __launch_bounds__(64) void refine_orient_kernel(RefArgs A) {
     for (int m = 0; m < 5; ++m) {
       const int t = q + 8 * m;
       ang[m] = 0.f;
-      if (t < kOriBins && R.ok) {
+      if (t < kOriBins && ok) {
         const int l = t > 0 ? t - 1 : kOriBins - 1;
         const int rr = t < kOriBins - 1 ? t + 1 : 0;
         const float h = sm[g][t], hl = sm[g][l], hr = sm[g][rr];
@@ -667,17 +722,10 @@ __global__ __launch_bounds__(64) void refine_orient_kernel(RefArgs A) {
         if (t < kOriBins && ((pmask >> t) & 1ull))
           co->angle[__popcll(pmask & ((1ull << t) - 1ull))] = ang[m];
       }
-      const int np = R.ok ? __popcll(pmask) : 0;
-      if (q == 0) {
-        co->x = R.x;
-        co->y = R.y;
-        co->size = R.size;
-        co->response = R.response;
-        co->octave = R.octave;
-        co->img = cd.b;
-        co->npeaks = np;
-        A.npeaks[ci] = np;
-      }
+      // co->npeaks keeps the refine pass's kept flag: other waves rank this
+      // chunk from it; the peak count goes to A.npeaks only
+      const int np = ok ? __popcll(pmask) : 0;
+      if (q == 0) A.npeaks[ci] = np;
     }
     wave_sync();
   }
@@ -698,7 +746,8 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.couts = D.couts;
   A.npeaks = D.npeaks;
   (void)batch;
-  hipLaunchKernelGGL(refine_orient_kernel, dim3(8192), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, st, A);
+  hipLaunchKernelGGL(orient_kernel, dim3(8192), dim3(64), 0, st, A);
 }
 
 // ---- ordered keypoint emission ------------------------------------------------
