@@ -475,6 +475,7 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
       dmalloc(&c->D.kp_scan, (size_t)cap + 1) != hipSuccess ||
       dmalloc(&c->D.kp_total, 1) != hipSuccess || dmalloc(&c->D.npeaks, (size_t)cap) != hipSuccess ||
       dmalloc(&c->D.scan_tmp, scan_n) != hipSuccess ||
+      dmalloc(&c->D.scan_tiles, (size_t)scan_tiles_for((long long)scan_n) + 1) != hipSuccess ||
       dmalloc(&c->d_img_off, max_batch + 1) != hipSuccess)
     return bail(SIFT_E_NOMEM);
   if (hipMemset(c->D.cand_total, 0, sizeof(int)) != hipSuccess) return bail(SIFT_E_HIP);
@@ -494,7 +495,7 @@ int sift_ctx_destroy(sift_ctx* c) {
   for (auto e : c->pool) (void)hipEventDestroy(e);
   void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
-                  c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->d_img_off,
+                  c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles, c->d_img_off,
                   c->d_kpts, c->d_desc, c->d_err, c->d_match};
   for (void* p : bufs)
     if (p) (void)hipFree(p);

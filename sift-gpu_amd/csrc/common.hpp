@@ -206,8 +206,10 @@ struct DetectBufs {
   int* kp_scan;         // per candidate exclusive scan of npeaks, [cand_cap+1]
   int* kp_total;        // [1]
   int* npeaks;          // orientation peaks per candidate, [cand_cap]
-  int* scan_tmp;        // scratch for the single-block scan
+  int* scan_tmp;        // exclusive scan of blk_counts, [blk_cap+1]
+  int* scan_tiles;      // per-tile sums of the multi-block scan, [scan_tiles_for(max(blk_cap, cand_cap))]
 };
+int scan_tiles_for(long long cap);
 long long mask_words_per_image(const Layout& L);
 int mask_blocks_per_image(const Layout& L);
 void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* dog, bool write_dog,

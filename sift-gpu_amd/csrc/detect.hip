@@ -291,54 +291,120 @@ __global__ __launch_bounds__(256) void mask_expand_kernel(MaskLayout M, const un
   }
 }
 
-// ---- single-workgroup exclusive scan -----------------------------------------
-// out[i] = sum(in[0..i)), out[n] = total.  n from n_dev (clamped to cap) if
-// given, else n_host.  Optional: img_out[b] = out[img_idx[b]] / out[b*stride].
-__global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ in, int in_stride,
-                                                    int* __restrict__ out, const int* n_dev,
-                                                    int n_host, int cap, int* total_out) {
+// ---- exclusive scan (reduce / scan of tile sums / down-sweep) ---------------
+// out[i] = sum(in[0..i)), out[n] = total (also *total_out if given).  n from
+// n_dev (clamped to cap) if given, else n_host.  The grid is sized from cap on
+// the host; tiles past n contribute 0 and write nothing.
+constexpr int kScanT = 256, kScanPer = 16, kScanTile = kScanT * kScanPer;
+
+__device__ __forceinline__ int scan_n(const int* n_dev, int n_host, int cap) {
+  const int n = n_dev ? *n_dev : n_host;
+  return n < cap ? n : cap;
+}
+
+__device__ __forceinline__ int block_sum(int v, int* red) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  int t = 0;
+  for (int k = 0; k < kScanT / 64; ++k) t += red[k];
+  return t;
+}
+
+__global__ __launch_bounds__(kScanT) void scan_reduce_kernel(const int* __restrict__ in, const int* n_dev,
+                                                             int n_host, int cap, int* __restrict__ tsum) {
+  __shared__ int red[kScanT / 64];
+  const int n = scan_n(n_dev, n_host, cap);
+  const long long base = (long long)blockIdx.x * kScanTile;
+  int s = 0;
+  if (base < n)
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const long long i = base + k * kScanT + threadIdx.x;
+      s += i < n ? in[i] : 0;
+    }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = s;
+}
+
+// exclusive scan of the tile sums in place (one workgroup); out[n] = total
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(int* __restrict__ tsum, int ntiles, const int* n_dev,
+                                                          int n_host, int cap, int* __restrict__ out,
+                                                          int* total_out) {
   __shared__ int wsum[16];
   __shared__ int carry_s;
-  int n = n_dev ? *n_dev : n_host;
-  if (n > cap) n = cap;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) carry_s = 0;
   __syncthreads();
-  for (int base = 0; base < n; base += 4096) {
-    int v[4];
-    int s = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = base + tid * 4 + k;
-      v[k] = i < n ? in[(long long)i * in_stride] : 0;
-      s += v[k];
-    }
-    int incl = s;  // inclusive wave scan
+  for (int base = 0; base < ntiles; base += 1024) {
+    const int i = base + tid;
+    const int v = i < ntiles ? tsum[i] : 0;
+    int incl = v;
     for (int off = 1; off < 64; off <<= 1) {
       const int t = __shfl_up(incl, off);
       if (lane >= off) incl += t;
     }
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    int wbefore = 0;
-    for (int k = 0; k < wv; ++k) wbefore += wsum[k];
-    int tot = 0;
-    for (int k = 0; k < 16; ++k) tot += wsum[k];
-    int run = carry_s + wbefore + incl - s;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = base + tid * 4 + k;
-      if (i < n) out[i] = run;
-      run += v[k];
+    int wbefore = 0, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      wbefore += k < wv ? wsum[k] : 0;
+      tot += wsum[k];
     }
+    if (i < ntiles) tsum[i] = carry_s + wbefore + incl - v;
     __syncthreads();
     if (tid == 0) carry_s += tot;
     __syncthreads();
   }
   if (tid == 0) {
-    out[n] = carry_s;
+    out[scan_n(n_dev, n_host, cap)] = carry_s;
     if (total_out) *total_out = carry_s;
   }
+}
+
+__global__ __launch_bounds__(kScanT) void scan_down_kernel(const int* __restrict__ in, const int* n_dev,
+                                                           int n_host, int cap, const int* __restrict__ tsum,
+                                                           int* __restrict__ out) {
+  __shared__ int wsum[kScanT / 64];
+  const int n = scan_n(n_dev, n_host, cap);
+  const long long base = (long long)blockIdx.x * kScanTile;
+  if (base >= n) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // thread tid owns the kScanPer consecutive elements [base + tid*kScanPer, ...)
+  int v[kScanPer];
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const long long i = base + (long long)tid * kScanPer + k;
+    v[k] = i < n ? in[i] : 0;
+    s += v[k];
+  }
+  int incl = s;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(incl, off);
+    if (lane >= off) incl += t;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int run = tsum[blockIdx.x] + incl - s;
+  for (int k = 0; k < wv; ++k) run += wsum[k];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const long long i = base + (long long)tid * kScanPer + k;
+    if (i < n) out[i] = run;
+    run += v[k];
+  }
+}
+
+int scan_tiles_for(long long cap) { return (int)((cap + kScanTile - 1) / kScanTile); }
+
+void launch_scan(hipStream_t st, const int* in, int* out, const int* n_dev, int n_host, int cap, int* total_out,
+                 int* tsum) {
+  const int nt = scan_tiles_for(cap) > 0 ? scan_tiles_for(cap) : 1;
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3(nt), dim3(kScanT), 0, st, in, n_dev, n_host, cap, tsum);
+  hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, st, tsum, nt, n_dev, n_host, cap, out, total_out);
+  hipLaunchKernelGGL(scan_down_kernel, dim3(nt), dim3(kScanT), 0, st, in, n_dev, n_host, cap, tsum, out);
 }
 
 // out[b] = scan[b*stride] (idx == nullptr) or scan[min(idx[b], n)] with n the
@@ -409,8 +475,7 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
   hipLaunchKernelGGL(mask_count_kernel, dim3(M.bpw, batch), dim3(256), 0, st, D.mask, M.w_img, M.bpw,
                      D.blk_counts);
   const int nblk = M.bpw * batch;
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, D.blk_counts, 1, D.scan_tmp, nullptr,
-                     nblk, nblk, D.cand_total);
+  launch_scan(st, D.blk_counts, D.scan_tmp, nullptr, nblk, nblk, D.cand_total, D.scan_tiles);
   hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(128), 0, st, D.scan_tmp, nullptr, M.bpw,
                      batch, nullptr, 0, D.img_cand_off);
   hipLaunchKernelGGL(mask_expand_kernel, dim3(M.bpw, batch), dim3(256), 0, st, M, D.mask, D.scan_tmp,
@@ -781,8 +846,7 @@ __global__ __launch_bounds__(256) void emit_kernel(const CandOut* __restrict__ c
 void launch_emit(hipStream_t st, DetectBufs& D, int batch, sift_keypoint* kpts, int kp_cap,
                  int* img_kp_off) {
   // kp_scan = exclusive scan of npeaks over the (clamped) candidate list
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, D.npeaks, 1, D.kp_scan,
-                     D.cand_total, 0, D.cand_cap, D.kp_total);
+  launch_scan(st, D.npeaks, D.kp_scan, D.cand_total, 0, D.cand_cap, D.kp_total, D.scan_tiles);
   hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(128), 0, st, D.kp_scan, D.img_cand_off,
                      0, batch, D.cand_total, D.cand_cap, img_kp_off);
   hipLaunchKernelGGL(emit_kernel, dim3(1024), dim3(256), 0, st, D.couts, D.kp_scan, D.cand_total,
