@@ -716,12 +716,24 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
     nmax = max(nmax, __shfl_xor(nmax, 16));
     nmax = max(nmax, __shfl_xor(nmax, 32));
     wave_sync();
+    // lane q walks samples s = q, q+8, ... as (row si, column sj) of the window
+    const int Dw = ns ? D : 0x40000000;  // rejected: never wraps
+    int si = 0, sj = q;
+    while (sj >= Dw) {
+      sj -= Dw;
+      ++si;
+    }
     for (int base = 0; base < nmax; base += 8) {
       const int s = base + q;
       int bin = -1;
       float val = 0.f;
+      const int i = si - radius, j = sj - radius;
+      sj += 8;
+      while (sj >= Dw) {
+        sj -= Dw;
+        ++si;
+      }
       if (s < ns) {
-        const int i = s / D - radius, j = s % D - radius;
         const int y = rr + i, x = rc + j;
         if (!(y <= 0 || y >= O.rows - 1) && !(x <= 0 || x >= O.cols - 1)) {
           const float2 mo = gimg[(long long)y * pitch + x];  // (Mag, Ori) of the pixel
