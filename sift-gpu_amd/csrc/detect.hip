@@ -640,6 +640,7 @@ __global__ __launch_bounds__(256) void refine_kernel(RefArgs A) {
 // takes 8 consecutive ranks, as in descriptor.hip.
 constexpr int kOGrp = 8;
 constexpr int kOChunk = 64;
+constexpr int kOU = 4;  // sample batches per loop step
 
 __device__ __forceinline__ void ohist_add(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -723,32 +724,37 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
       sj -= Dw;
       ++si;
     }
-    for (int base = 0; base < nmax; base += 8) {
-      const int s = base + q;
-      int bin = -1;
-      float val = 0.f;
-      const int i = si - radius, j = sj - radius;
-      sj += 8;
-      while (sj >= Dw) {
-        sj -= Dw;
-        ++si;
-      }
-      if (s < ns) {
-        const int y = rr + i, x = rc + j;
-        if (!(y <= 0 || y >= O.rows - 1) && !(x <= 0 || x >= O.cols - 1)) {
-          const float2 mo = gimg[(long long)y * pitch + x];  // (Mag, Ori) of the pixel
-          const float w = exp32f((i * i + j * j) * escale, etab, ek);
-          const float ori = mo.y;
-          const float mag = mo.x;
-          bin = cv_round((kOriBins / 360.f) * ori);
-          if (bin >= kOriBins) bin -= kOriBins;
-          if (bin < 0) bin += kOriBins;
-          val = w * mag;
+    // kOU batches of 8 samples per step: the kOU gathers are issued together
+    // (branch-free, clamped address), then the adds run in sample order
+    for (int base = 0; base < nmax; base += 8 * kOU) {
+      float2 mo[kOU];
+      int ii[kOU], jv[kOU];
+      bool okv[kOU];
+#pragma unroll
+      for (int u = 0; u < kOU; ++u) {
+        const int i = si - radius, j = sj - radius;
+        sj += 8;
+        while (sj >= Dw) {
+          sj -= Dw;
+          ++si;
         }
+        const int y = rr + i, x = rc + j;
+        okv[u] = base + 8 * u + q < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
+        ii[u] = i;
+        jv[u] = j;
+        mo[u] = gimg[okv[u] ? (long long)y * pitch + x : 0];  // (Mag, Ori) of the pixel
       }
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj)
-        if (q == jj && bin >= 0) ohist_add(&oh[g][bin], val);
+      for (int u = 0; u < kOU; ++u) {
+        const float w = exp32f((ii[u] * ii[u] + jv[u] * jv[u]) * escale, etab, ek);
+        int bin = cv_round((kOriBins / 360.f) * mo[u].y);
+        if (bin >= kOriBins) bin -= kOriBins;
+        if (bin < 0) bin += kOriBins;
+        const float val = w * mo[u].x;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+          if (q == jj && okv[u]) ohist_add(&oh[g][bin], val);
+      }
     }
     wave_sync();
     // smoothing (src/sift.cpp:440-451), max, peaks (src/sift.cpp:524-541)
