@@ -70,8 +70,8 @@ __device__ __forceinline__ void slab(float a, float b, int& lo, int& hi) {
 
 __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
-  // per-sample hand-off records: [sample j][group][owner q] = (bin address, value),
-  // row stride kRecStride2 words (conflict-free b128 stores, b64 loads)
+  // per-sample hand-off records: [sample j][group][owner q] = (bin qidx, value),
+  // row stride kRecStride2 words
   __shared__ __attribute__((aligned(16))) float rec[8 * kRecStride2];
   __shared__ int rows_tab[kGrp][kMaxWinRows];       // per row: (jlo + 64) | len << 16
   __shared__ float bc[kGrp][4];
@@ -213,11 +213,13 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
     //
     // The sample's lane resolves ownership for all 8 owners: with
     // (R0, C0, O0) = (r0+1, c0+1, o0) and odd = parity bits of the base bin,
-    // owner q receives corner k = q ^ odd (so corner values are XOR-permuted by
-    // odd in three swap layers) into bin index
-    //   qi(q) = qi0 + [R0 odd and q_r = 0]*15 + [C0 odd and q_c = 0]*5 + [O0 odd and q_o = 0].
-    float4 rc_cur[4];  // (addr, val) x 8 owners of this lane's sample
-    auto sample = [&](bool in_range, float4 (&out)[4]) {
+    // corner k = dr*4 + dc*2 + do lands in bin (R0+dr, C0+dc, O0+do), whose
+    // parity -- its owner -- is k ^ odd, at bin index
+    //   qidx_k = qi0 + [dr and R0 odd]*15 + [dc and C0 odd]*5 + [do and O0 odd].
+    // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
+    // the owner adds its lane to form the [qidx][lane] address.
+    float4 rc_cur[4];  // (qidx, val) x 8 corners of this lane's sample
+    auto sample = [&](bool in_range, float4 (&out)[4], int& odd_out) {
       const int i = ri - radius, j = rlo + u;
       const float c_rot = j * cos_t - i * sin_t;
       const float r_rot = j * sin_t + i * cos_t;
@@ -254,68 +256,72 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       v[0] = v_rc00 - v[1];
       const int R0 = ok ? r0 + 1 : 0, C0 = ok ? c0 + 1 : 0, O0 = ok ? o0 : 0;
       const int odd = ((R0 & 1) << 2) | ((C0 & 1) << 1) | (O0 & 1);
-      // w[q] = v[q ^ odd]: three conditional swap layers
-#define SWAP_LAYER(bit, s)                                 \
-  if (odd & (bit)) {                                       \
-    _Pragma("unroll") for (int t = 0; t < 8; ++t) {        \
-      if (!(t & (bit))) {                                  \
-        const float x = v[t];                              \
-        v[t] = v[t + (s)];                                 \
-        v[t + (s)] = x;                                    \
-      }                                                    \
-    }                                                      \
-  }
-      SWAP_LAYER(1, 1)
-      SWAP_LAYER(2, 2)
-      SWAP_LAYER(4, 4)
-#undef SWAP_LAYER
-      const int base0 = ((R0 >> 1) * 15 + (C0 >> 1) * 5 + (O0 >> 1)) * 64 + g * 8;
-      const int t15 = (odd & 4) ? 15 * 64 : 0, t5 = (odd & 2) ? 5 * 64 : 0, t1 = (odd & 1) ? 64 : 0;
+      // corner k's bin index qidx_k (independent of the owner); the store
+      // places it in owner slot k ^ odd, so no value permutation here
+      const int qi0 = (R0 >> 1) * 15 + (C0 >> 1) * 5 + (O0 >> 1);
+      const int a15 = (R0 & 1) ? 15 : 0, a5 = (C0 & 1) ? 5 : 0, a1 = O0 & 1;
+      const int q1 = qi0 + a1, q2 = qi0 + a5, q4 = qi0 + a15;
+      const int qk[8] = {qi0, q1, q2, q2 + a1, q4, q4 + a1, q4 + a5, q4 + a5 + a1};
 #pragma unroll
-      for (int oq = 0; oq < 8; ++oq) {
-        const int addr = base0 + oq + ((oq & 4) ? 0 : t15) + ((oq & 2) ? 0 : t5) + ((oq & 1) ? 0 : t1);
-        if (oq & 1) {
-          out[oq >> 1].z = __int_as_float(addr);
-          out[oq >> 1].w = v[oq];
-        } else {
-          out[oq >> 1].x = __int_as_float(addr);
-          out[oq >> 1].y = v[oq];
-        }
-      }
+      for (int t = 0; t < 4; ++t)
+        out[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
+                             v[2 * t + 1]);
+      odd_out = odd;
     };
+    // Entry ri+1 of the row table rides in a register (loaded one advance
+    // ahead), so the common advance -- at most one row change -- is
+    // branch-free selects with no LDS round trip; short or empty rows fall
+    // back to the row walk under a wave-uniform branch.
+    int enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
     auto advance = [&]() {  // to candidate sample t + 8
       u += 8;
-      while (ri < D && u >= rlen) {
-        u -= rlen;
-        if (++ri < D && table) {
-          const int e = rows_tab[g][ri];
-          rlo = (e & 0xffff) - 64;
-          rlen = e >> 16;
+      const bool mv = ri < D && u >= rlen;
+      u = mv ? u - rlen : u;
+      ri = mv ? ri + 1 : ri;
+      if (table) {
+        rlo = mv ? (enext & 0xffff) - 64 : rlo;
+        rlen = mv ? enext >> 16 : rlen;
+      }
+      if (__builtin_amdgcn_ballot_w64(ri < D && u >= rlen) != 0) {
+        while (ri < D && u >= rlen) {
+          u -= rlen;
+          if (++ri < D && table) {
+            const int e = rows_tab[g][ri];
+            rlo = (e & 0xffff) - 64;
+            rlen = e >> 16;
+          }
         }
       }
+      enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
     };
+    int odd_cur = 0;
     if (nmax > 0) {
-      sample(q < nsamp, rc_cur);
+      sample(q < nsamp, rc_cur, odd_cur);
       advance();
     }
     for (int base = 0; base < nmax; base += 8) {
-      float4* dst4 = reinterpret_cast<float4*>(rec + q * kRecStride2 + g * 16);
+      float2* dst2 = reinterpret_cast<float2*>(rec + q * kRecStride2 + g * 16);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) dst4[t] = rc_cur[t];
+      for (int t = 0; t < 4; ++t) {
+        dst2[(2 * t) ^ odd_cur] = make_float2(rc_cur[t].x, rc_cur[t].y);
+        dst2[(2 * t + 1) ^ odd_cur] = make_float2(rc_cur[t].z, rc_cur[t].w);
+      }
       wave_sync_d();
       float4 rc_nxt[4];
-      sample(base + 8 + q < nsamp, rc_nxt);
+      int odd_nxt = 0;
+      sample(base + 8 + q < nsamp, rc_nxt, odd_nxt);
       // ordered accumulation of batch k: lane q applies its record of each sample
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const float2 e = reinterpret_cast<const float2*>(rec + jj * kRecStride2)[lane];
-        const int a = __float_as_int(e.x);
+        const int a = (__float_as_int(e.x) << 6) + lane;
         hist[a] = hist[a] + e.y;
       }
       wave_sync_d();
       advance();
 #pragma unroll
       for (int t = 0; t < 4; ++t) rc_cur[t] = rc_nxt[t];
+      odd_cur = odd_nxt;
     }
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
     float cell[2][8];
