@@ -16,8 +16,11 @@
 //    every bin of parity q, so each sample hands exactly one corner to each
 //    lane and every bin is updated by one lane only, in sample order -- plain
 //    per-lane LDS read-modify-writes, no atomics, no cross-lane hazards.  The
-//    histogram lives at [qidx][lane] (qidx = (R>>1)*15 + (C>>1)*5 + (O>>1)),
-//    so all 64 lanes of an update hit distinct banks.
+//    histogram lives at [qidx][lane] (qidx = (R'>>1)*10 + (C'>>1)*5 + (O>>1)
+//    over the interior rows / columns R' = R-1, C' = C-1 in [0, 4) -- the only
+//    bins the fold reads; border-bin updates go to a trash row), so all 64
+//    lanes of an update hit distinct banks and a wave needs 5.4 KB, not
+//    11.5 KB (three waves per SIMD instead of two).
 //  * Fold, 0.2 clamp, uchar quantisation, RootSIFT (src/sift.cpp:676-721)
 //    keep the reference's sequential sums (lane 0 of the group).
 #include "common.hpp"
@@ -34,7 +37,8 @@ __device__ __forceinline__ void wave_sync_d() {
 
 constexpr int kGrp = 8;            // keypoints per wave
 constexpr int kChunk = 64;         // keypoints ranked together by window radius
-constexpr int kQBins = 45;         // bins per parity class: 3 x 3 x 5
+constexpr int kQBins = 21;         // bins per parity class: 2 x 2 x 5 interior + 1 trash
+constexpr int kTrash = 20;         // qidx of the discarded border bins
 constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
 constexpr int kRecStride2 = 132;   // words per sample row of the owner records (128 + pad)
 
@@ -212,10 +216,11 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
     // (exact no-op, every bin is >= +0) and gathers from a clamped address.
     //
     // The sample's lane resolves ownership for all 8 owners: with
-    // (R0, C0, O0) = (r0+1, c0+1, o0) and odd = parity bits of the base bin,
-    // corner k = dr*4 + dc*2 + do lands in bin (R0+dr, C0+dc, O0+do), whose
-    // parity -- its owner -- is k ^ odd, at bin index
-    //   qidx_k = qi0 + [dr and R0 odd]*15 + [dc and C0 odd]*5 + [do and O0 odd].
+    // (Rm, Cm, O0) = (r0, c0, o0) (interior coordinates, R' = R - 1) and odd =
+    // their parity bits, corner k = dr*4 + dc*2 + do lands in interior bin
+    // (Rm+dr, Cm+dc, O0+do), whose parity -- its owner -- is k ^ odd, at
+    //   qidx_k = qi0 + [dr and Rm odd]*10 + [dc and Cm odd]*5 + [do and O0 odd],
+    // or in the trash row when Rm+dr or Cm+dc leaves [0, 4).
     // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
     // the owner adds its lane to form the [qidx][lane] address.
     float4 rc_cur[4];  // (qidx, val) x 8 corners of this lane's sample
@@ -254,14 +259,19 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       v[2] = v_rc01 - v[3];
       v[1] = v_rc00 * obin;
       v[0] = v_rc00 - v[1];
-      const int R0 = ok ? r0 + 1 : 0, C0 = ok ? c0 + 1 : 0, O0 = ok ? o0 : 0;
-      const int odd = ((R0 & 1) << 2) | ((C0 & 1) << 1) | (O0 & 1);
+      // interior coordinates of the base corner: Rm = R0 - 1 = r0 in [-1, 3]
+      const int Rm = ok ? r0 : 0, Cm = ok ? c0 : 0, O0 = ok ? o0 : 0;
+      const int odd = ((Rm & 1) << 2) | ((Cm & 1) << 1) | (O0 & 1);
       // corner k's bin index qidx_k (independent of the owner); the store
       // places it in owner slot k ^ odd, so no value permutation here
-      const int qi0 = (R0 >> 1) * 15 + (C0 >> 1) * 5 + (O0 >> 1);
-      const int a15 = (R0 & 1) ? 15 : 0, a5 = (C0 & 1) ? 5 : 0, a1 = O0 & 1;
-      const int q1 = qi0 + a1, q2 = qi0 + a5, q4 = qi0 + a15;
-      const int qk[8] = {qi0, q1, q2, q2 + a1, q4, q4 + a1, q4 + a5, q4 + a5 + a1};
+      const int qi0 = (Rm >> 1) * 10 + (Cm >> 1) * 5 + (O0 >> 1);
+      const int a10 = (Rm & 1) ? 10 : 0, a5 = (Cm & 1) ? 5 : 0, a1 = O0 & 1;
+      const bool r0v = Rm >= 0, r1v = Rm <= 2, c0v = Cm >= 0, c1v = Cm <= 2;
+      const int q1 = qi0 + a1, q2 = qi0 + a5, q4 = qi0 + a10;
+      const int qk[8] = {r0v && c0v ? qi0 : kTrash,      r0v && c0v ? q1 : kTrash,
+                         r0v && c1v ? q2 : kTrash,       r0v && c1v ? q2 + a1 : kTrash,
+                         r1v && c0v ? q4 : kTrash,       r1v && c0v ? q4 + a1 : kTrash,
+                         r1v && c1v ? q4 + a5 : kTrash,  r1v && c1v ? q4 + a5 + a1 : kTrash};
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         out[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
@@ -328,11 +338,11 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       const int cidx = q + 8 * h2;
-      const int R = cidx / d + 1, C = cidx % d + 1;
+      const int R = cidx / d, C = cidx % d;  // interior coordinates R' = R-1, C' = C-1
 #pragma unroll
       for (int o = 0; o < nb + 2; ++o) {
         const int par = ((R & 1) << 2) | ((C & 1) << 1) | (o & 1);
-        const float hv = hist[((R >> 1) * 15 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
+        const float hv = hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
         if (o < nb)
           cell[h2][o] = hv;
         else
