@@ -118,8 +118,15 @@ __device__ __forceinline__ void blur_tile(const float* __restrict__ src, long lo
 #pragma unroll
     for (int b = 0; b < T::KS; ++b) {
       const float k = kr[b];
+      // all kPX products first (distinct registers, pinned by the empty asm),
+      // then the kPX adds: no multiply feeds the very next instruction
+      float t[kPX];
 #pragma unroll
-      for (int p = 0; p < kPX; ++p) acc[p] = acc[p] + win[p + b] * k;
+      for (int p = 0; p < kPX; ++p) t[p] = win[p + b] * k;
+      asm volatile("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]),
+                   "+v"(t[6]), "+v"(t[7]));
+#pragma unroll
+      for (int p = 0; p < kPX; ++p) acc[p] = acc[p] + t[p];
     }
   }
   const int y = y0 + ty;
