@@ -91,6 +91,34 @@ def test_dog_extrema_descriptors_bitexact(ctx, oracle):
     assert_bits_equal(ctx.calDescriptor(gpl, kps_ref, 0), desc_ref, "descriptors")
 
 
+def test_descriptors_caller_keypoints_bitexact(ctx, oracle):
+    """calDescriptor (src/sift.cpp:733-753) on caller-supplied keypoints: every
+    octave, layers 1-2, sub-pixel positions including the image border and
+    beyond it, angles 0 / near 360 / random, and sizes whose window radius
+    exceeds 40 (the whole-window enumeration path) -- windows that reach the
+    border cells and the trash row of the interior-only histogram."""
+    img = oracle.synth_image(11, 240, 320)
+    r, c = img.shape
+    g = oracle.build_gaussian_pyramid(img)
+    gpl = oracle.split_planes(g, r, c, 5, 5)
+    rng = np.random.default_rng(5)
+    n = 600
+    kps = np.zeros(n, oracle.KEYPOINT_DTYPE)
+    o = rng.integers(0, 5, n)
+    layer = rng.integers(1, 3, n)
+    size_oct = np.where(rng.random(n) < 0.25, rng.uniform(7.6, 12.0, n), rng.uniform(1.5, 7.0, n))
+    kps["x"] = rng.uniform(-3.0, c + 3.0, n).astype(np.float32)
+    kps["y"] = rng.uniform(-3.0, r + 3.0, n).astype(np.float32)
+    kps["size"] = (size_oct * (1 << o)).astype(np.float32)
+    ang = rng.uniform(0, 360, n).astype(np.float32)
+    ang[:40] = 0.0
+    ang[40:80] = np.nextafter(np.float32(360), np.float32(0))
+    kps["angle"] = ang
+    kps["octave"] = (o + (layer << 8)).astype(np.int32)
+    desc_ref = oracle.calc_descriptors(g, r, c, kps)
+    assert_bits_equal(ctx.calDescriptor(gpl, kps, 0), desc_ref, "descriptors")
+
+
 # ---- full SIFT_NCL ---------------------------------------------------------------
 GOLDEN_CASES = ["book", "synth0_160x128", "synth1_240x320", "synth2_203x157"]
 
