@@ -8,8 +8,16 @@ extrema + refinement + orientation, 128-D descriptors -- over one batch of
 BASELINE.json configs[2] at N=1; at N=8 the 8 x 64 = 512 images are
 configs[3]).  Inputs are generated on device (integer-exact generator,
 SURVEY.md 8(d) d2) before the timed region; every rank has its own images
-(weak scaling).  For N > 1 each step ends with the RCCL keypoint gather to
-rank 0 (sift-gpu_amd/sift_dist.py), the path's one exchange step.
+(weak scaling).  For N > 1 each step's keypoints are gathered to rank 0 over
+RCCL one step behind the compute (sift-gpu_amd/sift_dist.py), and the last
+step's gather is inside the timed region.
+
+Outside the timed region rank 0 checks its image 0 (seed 0) -- and seeds 31
+and 63 at the default shape -- against the CPU path's SHA-256 digests
+(tests/golden) and reports "output_verified".  Further legs (rank 0, N=1
+unless noted): SIFT_FLAG_FAST (separable pyramid, HBM roofline), configs[1]
+single-image latency (hipGraph replay, 4 octaves), the knnMatch leg, and the
+CPU baseline (oracle, 1 thread + image-parallel on the host's cores).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).  Rank 0 prints one JSON line.
@@ -17,11 +25,15 @@ torch.distributed.run (one rank per GPU, RCCL).  Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
+import numpy as np
 import torch  # first: its HIP runtime becomes the process-wide one
 import torch.distributed as dist
 
@@ -31,8 +43,11 @@ import siftgpu  # noqa: E402
 import sift_dist  # noqa: E402
 
 METRIC = "Mpix/s + keypoints/s, 1920×1080 grayscale, 1/2/4/8 MI355X vs CPU ref"
-FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = dense f32 MFMA peak
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector peak (FMA = 2 flops, 2-cycle wave64 issue)
+VALU_OP_PEAK_T = 78.65     # non-FMA fp32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
 
 
 def parse():
@@ -48,17 +63,41 @@ def parse():
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-fast", action="store_true", help="skip the SIFT_FLAG_FAST leg")
     p.add_argument("--no-match", action="store_true", help="skip the knnMatch leg (SURVEY 8(f) f2)")
+    p.add_argument("--no-single", action="store_true", help="skip the configs[1] single-image leg")
+    p.add_argument("--only", default=None, choices=[None, "exact", "fast", "single"],
+                   help="profiling runs: time only this leg")
     p.add_argument("--profile-json", default=None, help="also write per-stage stats here")
     return p.parse_args()
 
 
-def cpu_baseline(rows, cols, threads=1):
-    """Oracle (C restatement of the reference CPU path) on one image.  threads > 1
-    uses the reference's own OpenMP split (the descriptor loop, src/sift.cpp
-    calDescriptor); the rest of the path is serial there too."""
+# ---- CPU baseline (oracle = C restatement of the reference path) ------------
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # the checker / CPU baseline only
     O.build()
+    return O
+
+
+ORACLE_NOTE = ("oracle/sift_oracle.c: SIFT_NCL restated in C, gcc -O3 -ffp-contract=off, no -march "
+               "(reference makefile:25 flags); its blur tests the zero-padding bounds inline instead of "
+               "copying each ksize^2 neighbourhood through getSubMatrix (src/sift.cpp:110-120), so it is "
+               "faster than the reference's own loop (conservative for speed-up claims)")
+
+
+def cpu_baseline(rows, cols, threads=1):
+    """One image, `threads` OpenMP threads (the reference's own split: the
+    descriptor loop, src/sift.cpp:738; the rest of the path is serial there)."""
+    O = _oracle()
     O.set_threads(threads)
     img = O.synth_image(0, rows, cols)
     t0 = time.perf_counter()
@@ -68,12 +107,159 @@ def cpu_baseline(rows, cols, threads=1):
     mpix = rows * cols / 1e6
     return {"value": round(mpix / dt, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
             "keypoints_per_s": round(len(kps) / dt, 1), "seconds": round(dt, 3),
-            "sample": f"1 synthetic {cols}x{rows} image (seed 0), full SIFT_NCL restated in C "
-                      f"(oracle/sift_oracle.c, gcc -O2 -ffp-contract=off), {threads} thread(s)"
+            "sample": f"1 synthetic {cols}x{rows} image (seed 0), {threads} thread(s)"
                       f"{' (OpenMP over descriptors, as the reference)' if threads > 1 else ''}, "
-                      f"{len(kps)} keypoints"}
+                      f"{len(kps)} keypoints",
+            "note": ORACLE_NOTE}
 
 
+_WORKER = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+import oracle as O
+O.set_threads(1)
+img = O.synth_image(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+t0 = time.perf_counter()
+k, _ = O.sift(img, 5)
+print(len(k), time.perf_counter() - t0)
+"""
+
+
+def cpu_baseline_parallel(rows, cols, workers):
+    """Image-parallel all-cores rate: `workers`
+    independent processes, one image each, one thread each; rate = images /
+    wall.  Child processes import only the oracle (no GPU)."""
+    O = _oracle()
+    del O
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen([sys.executable, "-c", _WORKER, os.path.join(ROOT, "oracle"), str(100 + i),
+                               str(rows), str(cols)], stdout=subprocess.PIPE, text=True,
+                              env=dict(os.environ, OMP_NUM_THREADS="1", HIP_VISIBLE_DEVICES="",
+                                       CUDA_VISIBLE_DEVICES=""))
+             for i in range(workers)]
+    outs = [p.communicate(timeout=600)[0].split() for p in procs]
+    wall = time.perf_counter() - t0
+    if any(p.returncode for p in procs):
+        return None
+    nkp = sum(int(o[0]) for o in outs)
+    per_img = [float(o[1]) for o in outs]
+    mpix = workers * rows * cols / 1e6
+    return {"value": round(mpix / wall, 4), "unit": "Mpix/s", "cores": workers, "kind": "port",
+            "keypoints_per_s": round(nkp / wall, 1), "seconds_wall": round(wall, 3),
+            "seconds_per_image_median": round(float(np.median(per_img)), 3),
+            "sample": f"{workers} synthetic {cols}x{rows} images (seeds 100..{99 + workers}), one process and "
+                      f"one thread per image, all started together",
+            "note": ORACLE_NOTE}
+
+
+# ---- output check -----------------------------------------------------------
+def _sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def verify_outputs(kpts, desc, offs, R, C, B, octaves, seed_base):
+    """Digest check of this rank's outputs against the CPU path's
+    (tests/golden/make_golden.py).  Returns (verified seeds, failures)."""
+    if octaves != 5 or (R, C) != (1080, 1920):
+        return [], ["no golden digests for this shape / octave count"]
+    gold = {}
+    g0 = np.load(os.path.join(GOLDEN, "synth0_1080x1920.npz"), allow_pickle=False)
+    gold[0] = (int(g0["n"]), str(g0["kp_sha"]), str(g0["desc_sha"]))
+    gb = np.load(os.path.join(GOLDEN, "batch_1080x1920.npz"), allow_pickle=False)
+    for s, n, ks, ds in zip(gb["seeds"], gb["n"], gb["kp_sha"], gb["desc_sha"]):
+        gold[int(s)] = (int(n), str(ks), str(ds))
+    o = offs.cpu().numpy().astype(np.int64)
+    ok, bad = [], []
+    for seed, (n, ks, ds) in sorted(gold.items()):
+        b = seed - seed_base
+        if not 0 <= b < B:
+            continue
+        a, e = int(o[b]), int(o[b + 1])
+        k = kpts[a:e].cpu().numpy()
+        d = desc[a:e].cpu().numpy()
+        if e - a == n and _sha(k) == ks and _sha(d) == ds:
+            ok.append(seed)
+        else:
+            bad.append(seed)
+    return ok, bad
+
+
+def load_traffic():
+    try:
+        with open(TRAFFIC_JSON) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def traffic_of(tr, kernel):
+    k = tr.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["read_bytes"] + k["write_bytes"], tr.get("source")
+
+
+# ---- single image (configs[1]) ------------------------------------------------
+def single_image_leg(R, C, steps, warmup, octaves=4):
+    """configs[1]: one 1920x1080 image, 4 octaves x 5 scales.
+    device: image resident in HBM, sift_detect_compute_batch(batch 1) = the
+      captured hipGraph of the whole sequence, each call followed by
+      sift_sync (per-image latency incl. the wait);
+    host: SIFT_NCL from a host numpy image to host keypoints/descriptors
+      (upload, graphed compute, one wait for the count, one copy of n results)."""
+    out = {}
+    with siftgpu.Context(R, C, 1, device=torch.cuda.current_device()) as ctx:
+        ctx.set_octaves(octaves)
+        img = torch.empty((1, R, C), dtype=torch.float32, device="cuda")
+        ctx.synth_images(img.data_ptr(), 1, R, C, C, R * C, seed_base=0)
+        cap = 40000
+        kpts = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
+        desc = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
+        offs = torch.empty((2,), dtype=torch.int32, device="cuda")
+        for mode, flags in (("graph", 0), ("no_graph", siftgpu.SIFT_FLAG_NO_GRAPH)):
+            ctx.set_flags(flags)
+
+            def call():
+                ctx.detect_compute_batch(img.data_ptr(), 1, R, C, C, R * C, kpts.data_ptr(), desc.data_ptr(), cap,
+                                         offs.data_ptr())
+                ctx.sync()
+            for _ in range(warmup + 1):
+                call()
+            ts = []
+            for _ in range(max(steps, 10)):
+                t0 = time.perf_counter()
+                call()
+                ts.append(time.perf_counter() - t0)
+            out[f"device_{mode}_ms"] = round(float(np.median(ts)) * 1e3, 4)
+        n = int(offs[1].item())
+        ctx.set_flags(0)
+        host = img[0].cpu().numpy()
+        for _ in range(warmup + 1):
+            kps, dsc = ctx.SIFT_NCL(host)
+        ts = []
+        for _ in range(max(steps, 10)):
+            t0 = time.perf_counter()
+            kps, dsc = ctx.SIFT_NCL(host)
+            ts.append(time.perf_counter() - t0)
+        out["host_ms"] = round(float(np.median(ts)) * 1e3, 4)
+        gb = np.load(os.path.join(GOLDEN, "batch_1080x1920.npz"), allow_pickle=False)
+        verified = (R, C) == (1080, 1920) and octaves == 4 and len(kps) == int(gb["oct4_n"]) and \
+            _sha(kps) == str(gb["oct4_kp_sha"]) and _sha(dsc) == str(gb["oct4_desc_sha"])
+    lat = out["device_graph_ms"]
+    out.update({
+        "config": f"configs[1]: one {C}x{R} synthetic image (seed 0), {octaves} octaves x 5 scales, exact mode",
+        "keypoints": n, "output_verified": bool(verified),
+        "latency_ms": lat, "Mpix_per_s": round(R * C / 1e6 / (lat * 1e-3), 2),
+        "keypoints_per_s": round(n / (lat * 1e-3), 1),
+        "keypoints_per_s_host_to_host": round(n / (out["host_ms"] * 1e-3), 1),
+        "note": "latency = median wall time of one call + sift_sync, image resident in HBM; host_ms = "
+                "SIFT_NCL from host memory to host memory (H2D 8.3 MB, graphed compute, one wait, D2H of n "
+                "records); output_verified = the host call's keypoints/descriptors equal the CPU path's "
+                "(5-octave output filtered to octave <= 3, tests/golden/batch_1080x1920.npz)"})
+    return out
+
+
+# ---- knnMatch leg (SURVEY 8(f) f2) ---------------------------------------------
 def match_leg(ctx, a, desc, offs):
     """src/main.cpp:27 on the batch's own output: knnMatch(k=2) of image 1's
     descriptors (queries) against image 0's (train), device buffers, W + K
@@ -121,6 +307,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline and a.only is None:
+        # before this process touches the GPU: the image-parallel leg starts
+        # child processes
+        nthr = min(16, int(os.environ.get("OMP_NUM_THREADS", "16")))
+        cpu = {"cpu_baseline": cpu_baseline(a.rows, a.cols),
+               "cpu_baseline_omp": cpu_baseline(a.rows, a.cols, nthr)}
+        par = cpu_baseline_parallel(a.rows, a.cols, nthr)
+        if par:
+            cpu["cpu_baseline_all_cores"] = par
+        cpu["cpu_host"] = {"nproc": os.cpu_count(), "model": _cpu_model(), "share_used": nthr,
+                           "compiler_flags": "gcc -O3 -ffp-contract=off -fno-fast-math"}
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -132,19 +330,33 @@ def main():
     ctx = siftgpu.Context(R, C, B, device=dev, flags=siftgpu.SIFT_FLAG_PROFILE)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_octaves(a.octaves)
+    seed_base = rank * B
 
     imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
-    ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=rank * B)
+    ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=seed_base)
     cap = B * 40000
-    kpts = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
-    desc = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
-    offs = torch.empty((B + 1,), dtype=torch.int32, device="cuda")
+    gathering = world > 1 and not a.no_gather
+    nslots = 2 if gathering else 1
+    bufs = [(torch.empty((cap, 7), dtype=torch.int32, device="cuda"),
+             torch.empty((cap, 128), dtype=torch.float32, device="cuda"),
+             torch.empty((B + 1,), dtype=torch.int32, device="cuda")) for _ in range(nslots)]
+    runner = None
+    gathered = {"steps": 0, "keypoints": 0}
+    if gathering:
+        def on_result(step, out):
+            gathered["steps"] += 1
+            gathered["keypoints"] += sum(int(o[-1]) for o in out[1])
+        pipe = sift_dist.GatherPipeline(sift_dist.shard_sizes(world * B, world), cap, dst=0)
+        runner = sift_dist.PipelinedSteps(pipe, bufs, with_desc=False, on_result=on_result)
+
+    def compute(k, d, o):
+        ctx.detect_compute_batch(imgs.data_ptr(), B, R, C, C, R * C, k.data_ptr(), d.data_ptr(), cap, o.data_ptr())
 
     def step():
-        ctx.detect_compute_batch(imgs.data_ptr(), B, R, C, C, R * C, kpts.data_ptr(), desc.data_ptr(),
-                                 cap, offs.data_ptr())
-        if world > 1 and not a.no_gather:
-            sift_dist.gather_keypoints(kpts, offs, dst=0)
+        if runner is not None:
+            runner.step(compute)
+        else:
+            compute(*bufs[0])
 
     def leg(flags):
         """W warmup + K timed steps in one mode; returns (max-over-ranks seconds,
@@ -152,10 +364,9 @@ def main():
         ctx.set_flags(flags)
         for _ in range(a.warmup):
             step()
-        ctx.sync()  # checks device-side capacity flags
-        n_kp = int(offs[-1].item())
-        if n_kp > cap:
-            raise RuntimeError(f"keypoint capacity {cap} < {n_kp}")
+        if runner is not None:
+            runner.flush()
+        ctx.sync()  # sticky device status: candidate / keypoint capacity
         ctx.stage_stats(reset=True)
         if world > 1:
             dist.barrier()
@@ -163,69 +374,101 @@ def main():
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
+        if runner is not None:
+            runner.flush()   # the last step's gather is part of the timed work
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
+        ctx.sync()  # raises if any timed step overflowed a capacity
         stats = ctx.stage_stats(reset=True)
-        kp_step = torch.tensor([float(offs[-1].item())], dtype=torch.float64, device="cuda")
+        kp_step = torch.tensor([float(bufs[0][2][-1].item())], dtype=torch.float64, device="cuda")
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(kp_step, op=dist.ReduceOp.SUM)
         return float(t.item()), stats, float(kp_step.item())
 
-    dt, stats, kp_total_step = leg(siftgpu.SIFT_FLAG_PROFILE)
-    fast = None if a.no_fast else leg(siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
-    match = None if a.no_match or rank != 0 or B < 2 else match_leg(ctx, a, desc, offs)
+    want = (lambda leg_name: a.only in (None, leg_name))
+    exact = leg(siftgpu.SIFT_FLAG_PROFILE) if want("exact") else None
+    verified, failed = ([], [])
+    if exact is not None and rank == 0:
+        verified, failed = verify_outputs(*bufs[0], R, C, B, a.octaves, seed_base)
+    fast = None if (a.no_fast or not want("fast")) else leg(siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
+    match = None if (a.no_match or rank != 0 or B < 2 or exact is None) else match_leg(ctx, a, bufs[0][1], bufs[0][2])
+    single = None
+    if rank == 0 and world == 1 and not a.no_single and want("single"):
+        single = single_image_leg(R, C, a.steps, a.warmup)
 
     if rank == 0:
-        mpix = world * B * R * C * a.steps / 1e6
-        value = mpix / dt
-        # roofline of the dominant kernel: the exact octave blur (blur_octave_kernel)
-        bo = stats.get("blur_octave", {"ms": 0, "flops": 0, "bytes": 0, "launches": 0})
-        per_launch_ms = bo["ms"] / max(bo["launches"], 1)
-        tflops = (bo["flops"] / max(bo["launches"], 1)) / (per_launch_ms * 1e-3) / 1e12 if per_launch_ms else 0.0
-        roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": "blur_octave_kernel",
-                "avg_launch_ms": round(per_launch_ms, 4),
-                "note": "exact-mode 2-D blur is fp32-VALU bound (gfx950 fp32 vector peak = dense f32 MFMA "
-                        "peak = 157.3 TFLOP/s); the parity contract forbids FMA, so each tap is one "
-                        "multiply + one add instruction and the ceiling is frac 0.5; flops = 2 x taps "
-                        "per launch (one octave, 4 scales, whole batch)"}
-        pyr_ms = sum(stats[k]["ms"] for k in ("blur_base", "blur_octave", "decimate", "dog") if k in stats)
-        pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
-        out = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "Mpix/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(dt / a.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic: integer-exact 1920x1080 textures (SURVEY.md 8(d) d2) generated on device",
-            "config": {"workload": f"configs[2]: batch of {B} x {C}x{R} synthetic grayscale per GPU "
-                                   f"(N=8 x 64 = configs[3]), {a.octaves} octaves x 5 scales, exact mode",
-                       "global_batch": world * B, "rows": R, "cols": C, "octaves": a.octaves,
-                       "mode": "exact (bit-identical to the CPU path)",
-                       "parallelism": f"image-sharded x{world}" + (", RCCL keypoint gather" if world > 1 else "")},
-            "keypoints_per_s": round(kp_total_step * a.steps / dt, 1),
-            "keypoints_per_step": int(kp_total_step),
-            "roofline": roof,
-            "pyramid": {"ms_per_step": round(pyr_ms / a.steps, 3),
-                        "algorithmic_GBs": round(pyr_bytes / (pyr_ms * 1e-3) / 1e9, 1) if pyr_ms else None,
-                        "note": "B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes), SURVEY.md 8(d)"},
-            "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in stats.items()},
-        }
+        tr = load_traffic()
+        out = {"metric": METRIC}
+        if exact is not None:
+            dt, stats, kp_total_step = exact
+            mpix = world * B * R * C * a.steps / 1e6
+            value = mpix / dt
+            # roofline of the dominant kernel: the exact octave blur (blur_octave_kernel)
+            bo = stats.get("blur_octave", {"ms": 0, "flops": 0, "bytes": 0, "launches": 0})
+            per_launch_ms = bo["ms"] / max(bo["launches"], 1)
+            tflops = (bo["flops"] / max(bo["launches"], 1)) / (per_launch_ms * 1e-3) / 1e12 if per_launch_ms else 0.0
+            traffic, tsrc = traffic_of(tr, "blur_octave_kernel")
+            roof = {"bound": "valu", "achieved": round(tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                    "traffic_algorithmic": round(bo["bytes"] / max(bo["launches"], 1)),
+                    "traffic_source": tsrc,
+                    "kernel": "blur_octave_kernel",
+                    "avg_launch_ms": round(per_launch_ms, 4),
+                    "note": "exact-mode 2-D blur is fp32-VALU bound, no MFMA; peak = the fp32 vector peak "
+                            "(FMA counted as 2 flops); the parity contract forbids FMA, so each tap is one "
+                            "multiply + one add instruction and the ceiling is frac 0.5; flops = 2 x taps per "
+                            "launch (one octave, 4 scales, whole batch); traffic = HBM bytes per launch from "
+                            "the committed rocprofv3 PMC pass (calibrated FETCH_SIZE/WRITE_SIZE)"}
+            pyr_ms = sum(stats[k]["ms"] for k in ("blur_base", "blur_octave", "decimate", "dog") if k in stats)
+            pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
+            out.update({
+                "value": round(value, 2),
+                "unit": "Mpix/s",
+                "n_gpus": world,
+                "steps": a.steps,
+                "warmup": a.warmup,
+                "ms_per_step": round(dt / a.steps * 1e3, 3),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "f32",
+                "data": "synthetic: integer-exact 1920x1080 textures (SURVEY.md 8(d) d2) generated on device",
+                "config": {"workload": f"configs[2]: batch of {B} x {C}x{R} synthetic grayscale per GPU "
+                                       f"(N=8 x 64 = configs[3]), {a.octaves} octaves x 5 scales, exact mode",
+                           "global_batch": world * B, "rows": R, "cols": C, "octaves": a.octaves,
+                           "mode": "exact (bit-identical to the CPU path)",
+                           "parallelism": f"image-sharded x{world}" +
+                                          (", RCCL keypoint gather one step behind" if gathering else "")},
+                "output_verified": bool(verified) and not failed,
+                "output_verified_seeds": verified,
+                "keypoints_per_s": round(kp_total_step * a.steps / dt, 1),
+                "keypoints_per_step": int(kp_total_step),
+                "roofline": roof,
+                "pyramid": {"ms_per_step": round(pyr_ms / a.steps, 3),
+                            "algorithmic_GBs": round(pyr_bytes / (pyr_ms * 1e-3) / 1e9, 1) if pyr_ms else None,
+                            "note": "B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes), SURVEY.md 8(d)"},
+                "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in stats.items()},
+            })
+            if failed:
+                out["output_failed_seeds"] = failed
+            if gathering:
+                out["gather"] = {"steps_gathered": gathered["steps"],
+                                 "keypoints_gathered_per_step": gathered["keypoints"] / max(gathered["steps"], 1)}
+            d = stats.get("descriptor")
+            if d:
+                out["descriptor"] = {"ms_per_step": round(d["ms"] / a.steps, 3),
+                                     "keypoints_per_s_kernel": round(kp_total_step / world * a.steps /
+                                                                     (d["ms"] * 1e-3), 1)}
         if fast is not None:
             fdt, fst, fkp = fast
+            mpix = world * B * R * C * a.steps / 1e6
             pf = fst.get("pyramid_fast", {"ms": 0.0, "bytes": 0.0, "launches": 0})
             gbs = pf["bytes"] / (pf["ms"] * 1e-3) / 1e9 if pf["ms"] else 0.0
+            traffic, tsrc = traffic_of(tr, "pyr_fast_kernel")
             out["fast_mode"] = {
                 "value": round(mpix / fdt, 2), "unit": "Mpix/s", "ms_per_step": round(fdt / a.steps * 1e3, 3),
                 "keypoints_per_s": round(fkp * a.steps / fdt, 1), "keypoints_per_step": int(fkp),
@@ -236,7 +479,9 @@ def main():
                         "tests/test_gpu_fast.py"}
             out["roofline_pyramid_fast"] = {
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "pyr_fast_kernel",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_algorithmic": round(pf["bytes"] / max(pf["launches"], 1)),
+                "traffic_source": tsrc, "kernel": "pyr_fast_kernel",
                 "avg_launch_ms": round(pf["ms"] / max(pf["launches"], 1), 4),
                 "pyramid_ms_per_step": round(pf["ms"] / a.steps, 4),
                 "note": "algorithmic bytes B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes, "
@@ -250,24 +495,28 @@ def main():
                 "value": round(pairs / (match["ms"] * 1e-3) / 1e9, 3) if match["ms"] else None,
                 "unit": "Gpairs/s", "ms": round(match["ms"], 4),
                 "n_query": match["n_query"], "n_train": match["n_train"],
-                "roofline": {"bound": "valu", "achieved": round(lane_ops, 2), "peak": FP32_PEAK_TFLOPS / 2,
-                             "unit": "Tlane-op/s", "frac": round(lane_ops / (FP32_PEAK_TFLOPS / 2), 4),
+                "roofline": {"bound": "valu", "achieved": round(lane_ops, 2), "peak": VALU_OP_PEAK_T,
+                             "unit": "Tlane-op/s", "frac": round(lane_ops / VALU_OP_PEAK_T, 4),
                              "kernel": "knn_l1_kernel",
                              "note": "2 VALU lane-ops (v_sub, v_add |x|) per descriptor element per pair; "
                                      "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"},
                 "note": "SURVEY 8(f) f2 (src/main.cpp:25-27); bit-exact vs oracle/match.py"}
             if world == 1 and not a.no_cpu_baseline:
                 out["match"]["cpu_baseline"] = match_cpu_baseline(match)
-        if world == 1 and not a.no_cpu_baseline:
-            cb = cpu_baseline(R, C)
-            out["cpu_baseline"] = cb
-            nthr = min(16, int(os.environ.get("OMP_NUM_THREADS", "16")))
-            out["cpu_baseline_omp"] = cpu_baseline(R, C, nthr)
-            out["speedup_vs_cpu_1thread"] = {"Mpix/s": round(value / cb["value"], 1),
-                                             "keypoints/s": round(out["keypoints_per_s"] / cb["keypoints_per_s"], 1)}
-        if a.profile_json:
+        if single is not None:
+            out["single_image"] = single
+        if cpu is not None:
+            out.update(cpu)
+            cb = cpu["cpu_baseline"]
+            if exact is not None:
+                out["speedup_vs_cpu_1thread"] = {"Mpix/s": round(out["value"] / cb["value"], 1),
+                                                 "keypoints/s": round(out["keypoints_per_s"] / cb["keypoints_per_s"], 1)}
+            if single is not None:
+                single["speedup_vs_cpu_1thread_keypoints_per_s"] = round(
+                    single["keypoints_per_s"] / cb["keypoints_per_s"], 1)
+        if a.profile_json and exact is not None:
             with open(a.profile_json, "w") as f:
-                json.dump(stats, f, indent=1)
+                json.dump(exact[1], f, indent=1)
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:

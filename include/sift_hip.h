@@ -37,10 +37,17 @@ extern "C" {
 #define SIFT_E_CAPACITY (-3)  /* output capacity too small; required count reported */
 #define SIFT_E_SIZE (-4)      /* image/batch larger than the context was created for */
 #define SIFT_E_NOMEM (-5)     /* device allocation failed */
+#define SIFT_E_WORKSPACE (-6) /* the context's internal candidate workspace overflowed
+                                 (an input far more textured than the context was sized
+                                 for): no result is held, *n_out = -1; create the context
+                                 with a larger max size.  Not the two-call sizing case. */
 
 #define SIFT_FLAG_FAST 0x1u     /* separable fused pyramid (not bit-exact) */
 #define SIFT_FLAG_PROFILE 0x2u  /* per-stage HIP-event timing, see sift_get_stage_stats */
 #define SIFT_FLAG_VERBOSE 0x4u  /* print the reference's phase timings (src/sift.cpp:70,80,88) */
+#define SIFT_FLAG_NO_GRAPH 0x8u /* launch every kernel directly instead of replaying the context's
+                                   cached hipGraph of the compute sequence (graphs are also off
+                                   under SIFT_FLAG_PROFILE / SIFT_FLAG_VERBOSE) */
 
 #define SIFT_DESC_LEN 128
 #define SIFT_N_SCALES 5         /* Gaussian planes per octave */
@@ -75,7 +82,15 @@ void* sift_get_stream(sift_ctx* ctx);
 int sift_set_flags(sift_ctx* ctx, unsigned flags);
 /* Number of octaves (default 5, the literal at src/sift.cpp:67,68,78). */
 int sift_set_octaves(sift_ctx* ctx, int n_octaves);
+/* Waits for the context stream, then reports the sticky device status of the
+ * calls since the last report: SIFT_E_WORKSPACE (candidate workspace
+ * overflow), SIFT_E_CAPACITY (a batch call's keypoint total exceeded its
+ * kp_cap), SIFT_E_INVALID (calDescriptor's CV_Assert, src/sift.cpp:744). */
 int sift_sync(sift_ctx* ctx);
+/* Candidate (26-neighbour extremum) slots per image of the batch; the default
+ * is max(16384, max_rows * max_cols / 32), about 5x the extrema of a textured
+ * 1080p image.  Reallocates the workspace (synchronises). */
+int sift_set_candidate_capacity(sift_ctx* ctx, int per_image);
 const char* sift_version(void);
 
 /* ---- layout helpers ----------------------------------------------------- */

@@ -119,8 +119,18 @@ struct sift_ctx {
   int kp_cap = 0;
   int last_n = -1;                // keypoints held from the last host call
   bool last_has_desc = false;
-  int* d_err = nullptr;
+  int* d_err = nullptr;           // sticky error words [assert, workspace, kp capacity] (common.hpp)
+  int* d_stat = nullptr;          // status_kernel output: {candidates, keypoints, error word, 0}
+  int* h_stat = nullptr;          // pinned copy of d_stat, written at the end of every compute call
   void* d_match = nullptr;        // knn-match scratch (grown on demand)
+  // hipGraph cache of compute sequences (one per argument set; SIFT_FLAG_NO_GRAPH,
+  // _PROFILE and _VERBOSE run the launches directly)
+  struct GraphEntry {
+    std::vector<char> key;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+  };
+  std::vector<GraphEntry> graphs;
   size_t match_cap = 0;
   // profiling
   std::vector<StageRec> recs;
@@ -222,8 +232,11 @@ int ensure_coef_gen(sift_ctx* c, size_t n) {
   return SIFT_OK;
 }
 
+void drop_graphs(sift_ctx* c);
+
 int ensure_kp(sift_ctx* c, int need) {
   if (need <= c->kp_cap) return SIFT_OK;
+  drop_graphs(c);  // captured sequences name the old buffers
   if (c->d_kpts) (void)hipFree(c->d_kpts);
   if (c->d_desc) (void)hipFree(c->d_desc);
   c->d_kpts = nullptr;
@@ -233,6 +246,27 @@ int ensure_kp(sift_ctx* c, int need) {
   HIP_TRY(c, dmalloc(&c->d_desc, (size_t)need * kDescLen));
   c->kp_cap = need;
   return SIFT_OK;
+}
+
+// Candidate-list workspace for cap extrema (all images of a batch), plus the
+// internal keypoint buffer at 2 keypoints per candidate slot.
+int alloc_candidates(sift_ctx* c, int cap) {
+  drop_graphs(c);
+  void* old[] = {c->D.cands, c->D.couts, c->D.kp_scan, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles};
+  for (void* p : old)
+    if (p) (void)hipFree(p);
+  c->D.cands = nullptr;
+  c->D.couts = nullptr;
+  c->D.kp_scan = c->D.npeaks = c->D.scan_tmp = c->D.scan_tiles = nullptr;
+  c->D.cand_cap = 0;
+  const size_t scan_n = (size_t)std::max<long long>(c->blk_cap, cap) + 1;
+  if (dmalloc(&c->D.cands, (size_t)cap) != hipSuccess || dmalloc(&c->D.couts, (size_t)cap) != hipSuccess ||
+      dmalloc(&c->D.kp_scan, (size_t)cap + 1) != hipSuccess || dmalloc(&c->D.npeaks, (size_t)cap) != hipSuccess ||
+      dmalloc(&c->D.scan_tmp, scan_n) != hipSuccess ||
+      dmalloc(&c->D.scan_tiles, (size_t)scan_tiles_for((long long)scan_n) + 1) != hipSuccess)
+    return fail(c, SIFT_E_NOMEM, "candidate workspace allocation failed");
+  c->D.cand_cap = cap;
+  return ensure_kp(c, (int)std::min<long long>((long long)cap * 2, 1 << 28));
 }
 
 double plane_px(const Layout& L, int o) { return (double)L.oct[o].rows * L.oct[o].cols; }
@@ -311,20 +345,105 @@ void enqueue_desc(sift_ctx* c, const Layout& L, const sift_keypoint* kpts, const
                      first_octave, c->d_err);
 }
 
-// After a sync: device-side capacity / assertion checks.
-int check_device_status(sift_ctx* c) {
-  int ct = 0, e = 0;
-  HIP_TRY(c, hipMemcpy(&ct, c->D.cand_total, sizeof(int), hipMemcpyDeviceToHost));
-  HIP_TRY(c, hipMemcpy(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (ct > c->D.cand_cap)
-    return fail(c, SIFT_E_CAPACITY,
-                "candidate capacity " + std::to_string(c->D.cand_cap) + " < required " +
-                    std::to_string(ct) + " (create the context with a larger max size)");
-  if (e) {
-    HIP_TRY(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+// End of every compute sequence: status_kernel folds the candidate and
+// keypoint capacity checks into the sticky error word and the status block is
+// copied to pinned host memory on the same stream, so the host learns the
+// counts from the one stream synchronisation it already does.
+// img_off == nullptr: no keypoint count (calDescriptor); check_cand false: no
+// candidate check (no detection ran).
+void enqueue_status(sift_ctx* c, bool check_cand, const int* img_off, int batch, int kp_cap) {
+  launch_status(c->stream, check_cand ? c->D.cand_total : nullptr, c->D.cand_cap, img_off, batch, kp_cap, c->d_err,
+                c->d_stat);
+  (void)hipMemcpyAsync(c->h_stat, c->d_stat, 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream);
+}
+
+// After a stream sync: interprets the pinned status block of the last
+// compute call -- its own bits (sticky = false: host entry points) or every
+// bit not yet reported (sticky = true: sift_sync) -- restricted to mask, and
+// clears the device words of the bits it consumes.  kp_internal: keypoint
+// overflow of the context's own buffer is the caller's growth case.
+int take_status(sift_ctx* c, bool sticky, int mask, bool kp_internal = false) {
+  const int ct = c->h_stat[0], n = c->h_stat[1];
+  int e = (sticky ? c->h_stat[3] : c->h_stat[2]) & mask;
+  for (int i = 0; i < 3; ++i)
+    if (e & (1 << i)) HIP_TRY(c, hipMemsetAsync(c->d_err + i, 0, sizeof(int), c->stream));
+  c->h_stat[2] &= ~e;
+  c->h_stat[3] &= ~e;
+  if (kp_internal) e &= ~kErrKpCapacity;
+  if (!e) return SIFT_OK;
+  if (e & kErrWorkspace)
+    return fail(c, SIFT_E_WORKSPACE,
+                "candidate workspace overflow: capacity " + std::to_string(c->D.cand_cap) + " < " +
+                    std::to_string(ct) + " extrema (sift_set_candidate_capacity, or a larger context)");
+  if (e & kErrAssert)
     return fail(c, SIFT_E_INVALID,
                 "keypoint octave/layer outside the pyramid (CV_Assert at src/sift.cpp:744)");
+  return fail(c, SIFT_E_CAPACITY, "keypoint total " + std::to_string(n) +
+                                      " exceeds the output capacity (see d_img_offsets[batch])");
+}
+
+constexpr int kAllErr = kErrAssert | kErrWorkspace | kErrKpCapacity;
+
+// ---- hipGraph cache --------------------------------------------------------
+template <typename T>
+void key_put(std::vector<char>& k, const T& v) {
+  const char* p = reinterpret_cast<const char*>(&v);
+  k.insert(k.end(), p, p + sizeof(T));
+}
+
+void drop_graphs(sift_ctx* c) {
+  for (auto& g : c->graphs) {
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (g.graph) (void)hipGraphDestroy(g.graph);
   }
+  c->graphs.clear();
+}
+
+bool graphs_enabled(const sift_ctx* c) {
+  return !(c->flags & (SIFT_FLAG_PROFILE | SIFT_FLAG_VERBOSE | SIFT_FLAG_NO_GRAPH));
+}
+
+// Runs body() on the context stream: replayed from a cached hipGraph when one
+// was captured for the same key, captured now otherwise (direct launches if
+// graphs are off or capture fails).
+template <typename F>
+int run_graphed(sift_ctx* c, const std::vector<char>& key, F&& body) {
+  if (!graphs_enabled(c)) {
+    body();
+    HIP_TRY(c, hipGetLastError());
+    return SIFT_OK;
+  }
+  for (size_t i = 0; i < c->graphs.size(); ++i)
+    if (c->graphs[i].key == key) {
+      HIP_TRY(c, hipGraphLaunch(c->graphs[i].exec, c->stream));
+      return SIFT_OK;
+    }
+  sift_ctx::GraphEntry e;
+  e.key = key;
+  if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    body();
+    HIP_TRY(c, hipGetLastError());
+    return SIFT_OK;
+  }
+  body();
+  const hipError_t le = hipGetLastError();
+  const hipError_t ce = hipStreamEndCapture(c->stream, &e.graph);
+  if (le != hipSuccess || ce != hipSuccess || !e.graph ||
+      hipGraphInstantiate(&e.exec, e.graph, nullptr, nullptr, 0) != hipSuccess) {
+    if (e.graph) (void)hipGraphDestroy(e.graph);
+    (void)hipGetLastError();
+    body();  // capture failed: nothing ran, launch directly
+    HIP_TRY(c, hipGetLastError());
+    return SIFT_OK;
+  }
+  if (c->graphs.size() >= 4) {
+    (void)hipGraphExecDestroy(c->graphs.front().exec);
+    (void)hipGraphDestroy(c->graphs.front().graph);
+    c->graphs.erase(c->graphs.begin());
+  }
+  c->graphs.push_back(e);
+  HIP_TRY(c, hipGraphLaunch(e.exec, c->stream));
   return SIFT_OK;
 }
 
@@ -452,34 +571,28 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   MathConsts mc;
   host_math_consts(&mc);
   if (dmalloc(&c->d_coef, coefs.size()) != hipSuccess || dmalloc(&c->d_mc, 1) != hipSuccess ||
-      dmalloc(&c->d_err, 1) != hipSuccess)
+      dmalloc(&c->d_err, 4) != hipSuccess || dmalloc(&c->d_stat, 4) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_stat), 4 * sizeof(int), hipHostMallocDefault) != hipSuccess)
     return bail(SIFT_E_NOMEM);
+  memset(c->h_stat, 0, 4 * sizeof(int));
   if (hipMemcpy(c->d_coef, coefs.data(), coefs.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_mc, &mc, sizeof(mc), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess)
+      hipMemset(c->d_err, 0, 4 * sizeof(int)) != hipSuccess)
     return bail(SIFT_E_HIP);
   // detection workspace
   const long long px = (long long)max_rows * max_cols;
   const long long per_img = std::max<long long>(16384, px / 32);
   const long long cap = per_img * max_batch;
   if (cap > (1ll << 30)) return bail(SIFT_E_NOMEM);
-  c->D.cand_cap = (int)cap;
   c->blk_cap = mask_blocks_per_image(L) * max_batch;
-  const size_t scan_n = (size_t)std::max<long long>(c->blk_cap, cap) + 1;
   if (dmalloc(&c->D.mask, (size_t)mask_words_per_image(L) * max_batch) != hipSuccess ||
       dmalloc(&c->D.blk_counts, c->blk_cap) != hipSuccess ||
       dmalloc(&c->D.cand_total, 1) != hipSuccess ||
       dmalloc(&c->D.img_cand_off, max_batch + 1) != hipSuccess ||
-      dmalloc(&c->D.cands, (size_t)cap) != hipSuccess ||
-      dmalloc(&c->D.couts, (size_t)cap) != hipSuccess ||
-      dmalloc(&c->D.kp_scan, (size_t)cap + 1) != hipSuccess ||
-      dmalloc(&c->D.kp_total, 1) != hipSuccess || dmalloc(&c->D.npeaks, (size_t)cap) != hipSuccess ||
-      dmalloc(&c->D.scan_tmp, scan_n) != hipSuccess ||
-      dmalloc(&c->D.scan_tiles, (size_t)scan_tiles_for((long long)scan_n) + 1) != hipSuccess ||
-      dmalloc(&c->d_img_off, max_batch + 1) != hipSuccess)
+      dmalloc(&c->D.kp_total, 1) != hipSuccess || dmalloc(&c->d_img_off, max_batch + 1) != hipSuccess ||
+      alloc_candidates(c, (int)cap) != SIFT_OK)
     return bail(SIFT_E_NOMEM);
   if (hipMemset(c->D.cand_total, 0, sizeof(int)) != hipSuccess) return bail(SIFT_E_HIP);
-  if (ensure_kp(c, (int)std::min<long long>(cap * 2, 1 << 28)) != SIFT_OK) return bail(SIFT_E_NOMEM);
   *out = c;
   return SIFT_OK;
 }
@@ -493,7 +606,9 @@ int sift_ctx_destroy(sift_ctx* c) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : c->pool) (void)hipEventDestroy(e);
-  void* bufs[] = {c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
+  drop_graphs(c);
+  if (c->h_stat) (void)hipHostFree(c->h_stat);
+  void* bufs[] = {c->d_stat, c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
                   c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles, c->d_img_off,
                   c->d_kpts, c->d_desc, c->d_err, c->d_match};
@@ -512,6 +627,7 @@ int sift_set_stream(sift_ctx* c, void* s) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
   }
+  drop_graphs(c);  // captured on the old stream
   c->stream = (hipStream_t)s;
   c->own_stream = false;
   return SIFT_OK;
@@ -532,11 +648,21 @@ int sift_set_octaves(sift_ctx* c, int n) {
   return SIFT_OK;
 }
 
+int sift_set_candidate_capacity(sift_ctx* c, int per_image) {
+  if (!c) return SIFT_E_INVALID;
+  if (per_image < 1 || (long long)per_image * c->max_batch > (1ll << 30))
+    return fail(c, SIFT_E_INVALID, "candidate capacity out of range");
+  (void)hipSetDevice(c->device);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->last_n = -1;
+  return alloc_candidates(c, per_image * c->max_batch);
+}
+
 int sift_sync(sift_ctx* c) {
   if (!c) return SIFT_E_INVALID;
   (void)hipSetDevice(c->device);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  return check_device_status(c);
+  return take_status(c, true, kAllErr);
 }
 
 int sift_synth_images(sift_ctx* c, float* d_out, int batch, int rows, int cols, size_t row_stride,
@@ -569,6 +695,59 @@ int sift_copy_results(sift_ctx* c, sift_keypoint* kpts, float* desc, int cap, in
   return SIFT_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The whole SIFT_NCL device sequence for a batch (pyramid -> detect ->
+// descriptors -> status block), replayed from the context's hipGraph cache.
+int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols, size_t row_stride,
+                size_t img_stride, sift_keypoint* d_kpts, float* d_desc, int kp_cap, int* d_img_offsets) {
+  const Layout L = make_layout(rows, cols, c->n_oct);
+  const Plane src{d_imgs, (long long)row_stride, (long long)img_stride};
+  if (c->flags & SIFT_FLAG_VERBOSE) {
+    hipEvent_t v0 = get_event(c), v1 = get_event(c), v2 = get_event(c), v3 = get_event(c);
+    (void)hipEventRecord(v0, c->stream);
+    enqueue_pyramid(c, L, src, batch, false);
+    (void)hipEventRecord(v1, c->stream);
+    enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
+    (void)hipEventRecord(v2, c->stream);
+    enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
+    (void)hipEventRecord(v3, c->stream);
+    enqueue_status(c, true, d_img_offsets, batch, kp_cap);
+    verbose_phase(c, "pyramid construction time", v0, v1);
+    verbose_phase(c, "keypoint localization time", v1, v2);
+    verbose_phase(c, "descriptor extraction time", v2, v3);
+    c->pool.insert(c->pool.end(), {v0, v1, v2, v3});
+    HIP_TRY(c, hipGetLastError());
+    return SIFT_OK;
+  }
+  std::vector<char> key;
+  key_put(key, 1);  // sequence id
+  key_put(key, d_imgs);
+  key_put(key, batch);
+  key_put(key, rows);
+  key_put(key, cols);
+  key_put(key, row_stride);
+  key_put(key, img_stride);
+  key_put(key, d_kpts);
+  key_put(key, d_desc);
+  key_put(key, kp_cap);
+  key_put(key, d_img_offsets);
+  key_put(key, c->n_oct);
+  key_put(key, c->flags);
+  return run_graphed(c, key, [&]() {
+    enqueue_pyramid(c, L, src, batch, false);
+    enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
+    enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
+    enqueue_status(c, true, d_img_offsets, batch, kp_cap);
+  });
+}
+
+}  // namespace
+
+extern "C" {
+
 int sift_detect_compute_batch(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
                               size_t row_stride, size_t img_stride, sift_keypoint* d_kpts,
                               float* d_desc, int kp_cap, int* d_img_offsets) {
@@ -578,34 +757,17 @@ int sift_detect_compute_batch(sift_ctx* c, const float* d_imgs, int batch, int r
   if (!d_imgs || !d_kpts || !d_desc || !d_img_offsets || kp_cap < 0 || row_stride < (size_t)cols)
     return fail(c, SIFT_E_INVALID, "null buffer or bad stride");
   (void)hipSetDevice(c->device);
-  if (d_kpts == c->d_kpts) {
-    // internal buffers (host entry point): results are re-cached by the caller
-  } else {
-    c->last_n = -1;
-  }
-  const Layout L = make_layout(rows, cols, c->n_oct);
-  hipEvent_t v0 = nullptr, v1 = nullptr, v2 = nullptr, v3 = nullptr;
-  const bool verbose = c->flags & SIFT_FLAG_VERBOSE;
-  if (verbose) {
-    v0 = get_event(c), v1 = get_event(c), v2 = get_event(c), v3 = get_event(c);
-    (void)hipEventRecord(v0, c->stream);
-  }
-  enqueue_pyramid(c, L, Plane{d_imgs, (long long)row_stride, (long long)img_stride}, batch, false);
-  if (verbose) (void)hipEventRecord(v1, c->stream);
-  enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
-  if (verbose) (void)hipEventRecord(v2, c->stream);
-  enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
-  if (verbose) {
-    (void)hipEventRecord(v3, c->stream);
-    verbose_phase(c, "pyramid construction time", v0, v1);
-    verbose_phase(c, "keypoint localization time", v1, v2);
-    verbose_phase(c, "descriptor extraction time", v2, v3);
-    c->pool.insert(c->pool.end(), {v0, v1, v2, v3});
-  }
-  HIP_TRY(c, hipGetLastError());
-  return SIFT_OK;
+  c->last_n = -1;
+  return enqueue_ncl(c, d_imgs, batch, rows, cols, row_stride, img_stride, d_kpts, d_desc, kp_cap,
+                     d_img_offsets);
 }
 
+// SIFT_NCL from host memory: upload -> the graphed device sequence -> ONE
+// stream synchronisation (the status block, with the keypoint count, arrives
+// in pinned memory with it) -> one copy of exactly n results.  The internal
+// keypoint buffer is sized at creation for 2 keypoints per candidate slot;
+// a larger count (more than 2 orientation peaks per extremum on average)
+// grows it and runs again.
 int sift_detect_compute(sift_ctx* c, const float* img, int rows, int cols, size_t row_stride_bytes,
                         sift_keypoint* kpts, float* desc, int cap, int* n_out) {
   if (!c) return SIFT_E_INVALID;
@@ -614,14 +776,16 @@ int sift_detect_compute(sift_ctx* c, const float* img, int rows, int cols, size_
   int rc = check_dims(c, rows, cols, c->n_oct, 1);
   if (rc) return rc;
   (void)hipSetDevice(c->device);
+  c->last_n = -1;
+  *n_out = -1;
   if ((rc = upload_image(c, img, rows, cols, row_stride_bytes))) return rc;
   for (int attempt = 0; attempt < 2; ++attempt) {
-    rc = sift_detect_compute_batch(c, c->d_in, 1, rows, cols, c->in_pitch, c->in_img, c->d_kpts,
-                                   c->d_desc, c->kp_cap, c->d_img_off);
+    rc = enqueue_ncl(c, c->d_in, 1, rows, cols, c->in_pitch, c->in_img, c->d_kpts, c->d_desc, c->kp_cap,
+                     c->d_img_off);
     if (rc) return rc;
-    if ((rc = sift_sync(c))) return rc;
-    int n = 0;
-    HIP_TRY(c, hipMemcpy(&n, c->d_img_off + 1, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if ((rc = take_status(c, false, kAllErr, true))) return rc;
+    const int n = c->h_stat[1];
     if (n > c->kp_cap) {  // grow the internal buffer and run again
       if ((rc = ensure_kp(c, n))) return rc;
       continue;
@@ -638,8 +802,8 @@ int sift_detect_compute(sift_ctx* c, const float* img, int rows, int cols, size_
                                 c->stream));
       HIP_TRY(c, hipMemcpyAsync(desc, c->d_desc, sizeof(float) * kDescLen * n,
                                 hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return SIFT_OK;
   }
   return fail(c, SIFT_E_CAPACITY, "keypoint buffer growth failed");
@@ -747,12 +911,15 @@ int sift_find_scale_space_extrema(sift_ctx* c, const float* gpyr, const float* d
   const Layout L = make_layout(rows, cols, n_octaves);
   if ((rc = copy_pyramid(c, L, c->d_gpyr, gpyr, nullptr, kScales))) return rc;
   if ((rc = copy_pyramid(c, L, c->d_dog, dog, nullptr, kDogPer))) return rc;
+  c->last_n = -1;
+  *n_out = -1;
   for (int attempt = 0; attempt < 2; ++attempt) {
     enqueue_detect(c, L, 1, c->d_kpts, c->kp_cap, c->d_img_off, false);
+    enqueue_status(c, true, c->d_img_off, 1, c->kp_cap);
     HIP_TRY(c, hipGetLastError());
-    if ((rc = sift_sync(c))) return rc;
-    int n = 0;
-    HIP_TRY(c, hipMemcpy(&n, c->d_img_off + 1, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if ((rc = take_status(c, false, kAllErr, true))) return rc;
+    const int n = c->h_stat[1];
     if (n > c->kp_cap) {
       if ((rc = ensure_kp(c, n))) return rc;
       continue;
@@ -789,9 +956,10 @@ int sift_calc_descriptors(sift_ctx* c, const float* gpyr, int rows, int cols, in
   // keypoints may name any scale 0..4 (CV_Assert at src/sift.cpp:744): gradients of all five
   launch_grad(c->stream, L, c->d_gpyr, c->d_grad, 1, 0, kScales - 1, c->d_mc);
   enqueue_desc(c, L, c->d_kpts, c->d_img_off, 1, c->kp_cap, c->d_desc, first_octave);
+  enqueue_status(c, false, nullptr, 1, c->kp_cap);  // no detection ran: assertion bit only
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  if ((rc = check_device_status(c))) return rc;
+  if ((rc = take_status(c, false, kErrAssert))) return rc;
   HIP_TRY(c, hipMemcpy(desc, c->d_desc, sizeof(float) * kDescLen * n, hipMemcpyDeviceToHost));
   return SIFT_OK;
 }

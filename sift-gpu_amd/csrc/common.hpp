@@ -220,6 +220,13 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
                           const float* dog, const MathConsts* mc, DetectBufs& D, int batch);
 void launch_emit(hipStream_t st, DetectBufs& D, int batch, sift_keypoint* kpts, int kp_cap,
                  int* img_kp_off);
+// Device status bits; bit i <-> sticky error word err[i] (DescArgs::err_flag = &err[0],
+// status_kernel).
+constexpr int kErrAssert = 1;      // keypoint octave/layer outside the pyramid (CV_Assert)
+constexpr int kErrWorkspace = 2;   // candidate workspace overflow
+constexpr int kErrKpCapacity = 4;  // keypoint total above the output capacity
+void launch_status(hipStream_t st, const int* cand_total, int cand_cap, const int* img_off, int batch, int kp_cap,
+                   int* err, int* stat);
 
 // descriptor.hip
 void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, const MathConsts* mc,

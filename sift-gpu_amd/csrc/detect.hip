@@ -408,19 +408,23 @@ void launch_scan(hipStream_t st, const int* in, int* out, const int* n_dev, int 
 }
 
 // out[b] = scan[b*stride] (idx == nullptr) or scan[min(idx[b], n)] with n the
-// clamped length of the scanned list, for b = 0..batch.
+// clamped length of the scanned list, for b = 0..batch (any batch: the block
+// strides over it).
 __global__ void gather_offsets_kernel(const int* __restrict__ scan, const int* __restrict__ idx,
                                       int stride, int batch, const int* n_dev, int cap,
                                       int* __restrict__ out) {
-  const int b = threadIdx.x;
-  if (b > batch) return;
-  if (!idx) {
-    out[b] = scan[b * stride];
-  } else {
-    int n = *n_dev;
+  int n = 0;
+  if (idx) {
+    n = *n_dev;
     n = n < cap ? n : cap;
-    const int i = idx[b];
-    out[b] = scan[i < n ? i : n];
+  }
+  for (int b = threadIdx.x; b <= batch; b += blockDim.x) {
+    if (!idx) {
+      out[b] = scan[(long long)b * stride];
+    } else {
+      const int i = idx[b];
+      out[b] = scan[i < n ? i : n];
+    }
   }
 }
 
@@ -476,7 +480,7 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
                      D.blk_counts);
   const int nblk = M.bpw * batch;
   launch_scan(st, D.blk_counts, D.scan_tmp, nullptr, nblk, nblk, D.cand_total, D.scan_tiles);
-  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(128), 0, st, D.scan_tmp, nullptr, M.bpw,
+  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(256), 0, st, D.scan_tmp, nullptr, M.bpw,
                      batch, nullptr, 0, D.img_cand_off);
   hipLaunchKernelGGL(mask_expand_kernel, dim3(M.bpw, batch), dim3(256), 0, st, M, D.mask, D.scan_tmp,
                      D.cands, D.cand_cap);
@@ -861,11 +865,36 @@ __global__ __launch_bounds__(256) void emit_kernel(const CandOut* __restrict__ c
   }
 }
 
+// End-of-call status (one lane).  err[0..2] are sticky words (assertion,
+// candidate workspace overflow, keypoint capacity exceeded); this call's own
+// overflows are added to them.  stat = {candidates, keypoints, this call's
+// bits, all sticky bits} (bit i <-> err[i]), copied by the host to pinned
+// memory in the same stream, so it arrives with the stream synchronisation.
+__global__ void status_kernel(const int* __restrict__ cand_total, int cand_cap, const int* __restrict__ img_off,
+                              int batch, int kp_cap, int* __restrict__ err, int* __restrict__ stat) {
+  if (threadIdx.x != 0) return;
+  const int ct = cand_total ? *cand_total : 0;
+  const int n = img_off ? img_off[batch] : 0;
+  const int fresh = (err[0] ? kErrAssert : 0) | (ct > cand_cap ? kErrWorkspace : 0) | (n > kp_cap ? kErrKpCapacity : 0);
+  if (fresh & kErrWorkspace) err[1] = 1;
+  if (fresh & kErrKpCapacity) err[2] = 1;
+  stat[0] = ct;
+  stat[1] = n;
+  stat[2] = fresh;
+  stat[3] = (err[0] ? kErrAssert : 0) | (err[1] ? kErrWorkspace : 0) | (err[2] ? kErrKpCapacity : 0);
+}
+
+void launch_status(hipStream_t st, const int* cand_total, int cand_cap, const int* img_off, int batch, int kp_cap,
+                   int* err, int* stat) {
+  hipLaunchKernelGGL(status_kernel, dim3(1), dim3(64), 0, st, cand_total, cand_cap, img_off, batch, kp_cap, err,
+                     stat);
+}
+
 void launch_emit(hipStream_t st, DetectBufs& D, int batch, sift_keypoint* kpts, int kp_cap,
                  int* img_kp_off) {
   // kp_scan = exclusive scan of npeaks over the (clamped) candidate list
   launch_scan(st, D.npeaks, D.kp_scan, D.cand_total, 0, D.cand_cap, D.kp_total, D.scan_tiles);
-  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(128), 0, st, D.kp_scan, D.img_cand_off,
+  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(256), 0, st, D.kp_scan, D.img_cand_off,
                      0, batch, D.cand_total, D.cand_cap, img_kp_off);
   hipLaunchKernelGGL(emit_kernel, dim3(1024), dim3(256), 0, st, D.couts, D.kp_scan, D.cand_total,
                      D.cand_cap, kpts, kp_cap);

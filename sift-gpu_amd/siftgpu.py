@@ -32,7 +32,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libsift_hip.so")
 
 SIFT_OK, SIFT_E_INVALID, SIFT_E_HIP, SIFT_E_CAPACITY, SIFT_E_SIZE, SIFT_E_NOMEM = 0, -1, -2, -3, -4, -5
-SIFT_FLAG_FAST, SIFT_FLAG_PROFILE, SIFT_FLAG_VERBOSE = 0x1, 0x2, 0x4
+SIFT_E_WORKSPACE = -6  # internal candidate workspace overflow: an error, never the sizing case
+SIFT_FLAG_FAST, SIFT_FLAG_PROFILE, SIFT_FLAG_VERBOSE, SIFT_FLAG_NO_GRAPH = 0x1, 0x2, 0x4, 0x8
 N_SCALES, N_DOG, DESC_LEN = 5, 4, 128
 
 KEYPOINT_DTYPE = np.dtype(
@@ -81,6 +82,7 @@ def lib():
             "sift_set_flags": (ip, [vp, ctypes.c_uint]),
             "sift_set_octaves": (ip, [vp, ip]),
             "sift_sync": (ip, [vp]),
+            "sift_set_candidate_capacity": (ip, [vp, ip]),
             "sift_version": (ctypes.c_char_p, []),
             "sift_octave_shapes": (ip, [ip, ip, ip, pint, pint]),
             "sift_packed_size": (sz, [ip, ip, ip, ip]),
@@ -195,6 +197,9 @@ class Context:
 
     def sync(self):
         self._check("sift_sync", self._L.sift_sync(self.h))
+
+    def set_candidate_capacity(self, per_image: int):
+        self._check("sift_set_candidate_capacity", self._L.sift_set_candidate_capacity(self.h, per_image))
 
     # ---- host-memory API (reference names) ------------------------------
     def SIFT_NCL(self, img: np.ndarray):

@@ -1,6 +1,7 @@
 """Generate the committed golden fixtures under tests/golden/.
 
-Run from the repo root:  python tests/golden/make_golden.py
+Run from the repo root:  python tests/golden/make_golden.py   (--8k, --batch: the
+large-size digest sets)
 
 What is made, and from what:
   book_gray.pgm   data/book.jpg of the reference, decoded with PIL and converted
@@ -82,8 +83,34 @@ def case(name, img, with_planes=True, store_full=True):
     print(f"{name}: {r}x{c} -> {len(kps)} keypoints")
 
 
+def batch_1080():
+    """configs[2] / configs[1] check vectors: seeds 0, 31, 63 of the bench's
+    64-image 1080p batch (image b of bench.py's rank 0 is seed b), and seed
+    0 with 4 octaves (configs[1]), defined as the 5-octave output filtered to
+    octave <= 3 ('Config mismatch')."""
+    seeds = [0, 31, 63]
+    out = dict(seeds=np.array(seeds), rows=1080, cols=1920)
+    n, ks, ds = [], [], []
+    for b in seeds:
+        kps, desc = O.sift(O.synth_image(b, 1080, 1920), 5)
+        n.append(len(kps))
+        ks.append(hashlib.sha256(kps.tobytes()).hexdigest())
+        ds.append(hashlib.sha256(desc.tobytes()).hexdigest())
+        if b == 0:
+            keep = (kps["octave"] & 255) <= 3
+            out["oct4_n"] = int(keep.sum())
+            out["oct4_kp_sha"] = hashlib.sha256(kps[keep].tobytes()).hexdigest()
+            out["oct4_desc_sha"] = hashlib.sha256(np.ascontiguousarray(desc[keep]).tobytes()).hexdigest()
+        print(f"batch seed {b}: {len(kps)} keypoints")
+    out.update(n=np.array(n), kp_sha=np.array(ks), desc_sha=np.array(ds))
+    np.savez_compressed(os.path.join(OUT, "batch_1080x1920.npz"), **out)
+
+
 def main():
     O.build()
+    if "--batch" in sys.argv:
+        batch_1080()
+        return
     if "--8k" in sys.argv:
         # configs[4]: one 7680x4320 image (digests only; about 2 minutes of CPU)
         O.set_threads(os.cpu_count() or 1)

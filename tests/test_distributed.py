@@ -24,6 +24,11 @@ def test_shard_covers_every_image_once():
     assert sdist.shard(512, 8, 3) == (192, 256)   # C4: 64 images per GPU
 
 
+def test_shard_sizes():
+    assert sdist.shard_sizes(10, 4) == [2, 3, 2, 3]
+    assert sdist.shard_sizes(512, 8) == [64] * 8
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -56,9 +61,88 @@ def _worker(rank, world, port, q):
         out = sdist.gather_keypoints(kp, offs0, dst=0)
         if rank == 0:
             q.put([k.shape[0] for k in out[0]])
+        # uneven shards: 2 images on rank 0, 3 on rank 1
+        batches = [2, 3]
+        b = batches[rank]
+        nk = 4 + rank
+        offs_u = torch.tensor([0] + [min(nk, j + 1) for j in range(b - 1)] + [nk], dtype=torch.int32)
+        out = sdist.gather_keypoints(kp, offs_u, dst=0, batches=batches)
+        if rank == 0:
+            q.put(([k.shape[0] for k in out[0]], [o.tolist() for o in out[1]]))
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def _fake_step(rank, step, cap):
+    """Deterministic stand-in for one detect_compute_batch call of this rank."""
+    batch = [2, 3][rank]
+    per = [(step * 3 + rank * 5 + j) % 7 for j in range(batch)]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(per)]), dtype=torch.int32)
+    n = int(offs[-1])
+    kp = torch.arange(n * 7, dtype=torch.int32).reshape(n, 7) + 100000 * rank + 1000 * step
+    desc = torch.full((n, 128), float(step * 10 + rank))
+    return offs, kp, desc
+
+
+def _pipeline_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cap = 64
+        pipe = sdist.GatherPipeline(sdist.shard_sizes(5, world), cap, dst=0)
+        bufs = [(torch.zeros((cap, 7), dtype=torch.int32), torch.zeros((cap, 128)),
+                 torch.zeros(4, dtype=torch.int32)) for _ in range(2)]
+        got = {}
+
+        def on_result(step, out):
+            ks, offs, ds = out
+            got[step] = ([k.clone() for k in ks], [o.clone() for o in offs], [d.clone() for d in ds])
+
+        runner = sdist.PipelinedSteps(pipe, bufs, with_desc=True, on_result=on_result)
+        for step in range(5):
+            def compute(k, d, o, step=step):
+                offs, kp, desc = _fake_step(rank, step, cap)
+                o[:len(offs)] = offs
+                k[:len(kp)] = kp
+                d[:len(desc)] = desc
+            runner.step(compute)
+        runner.flush()
+        if rank == 0:
+            ok = sorted(got) == list(range(5))
+            for step in range(5):
+                for r in range(world):
+                    offs, kp, desc = _fake_step(r, step, cap)
+                    ks, os_, ds = got[step]
+                    ok = ok and torch.equal(ks[r], kp) and torch.equal(os_[r], offs) and torch.equal(ds[r], desc)
+            q.put(ok)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    return procs, q
+
+
+def test_pipelined_steps_world2_uneven():
+    """The bench's N > 1 step loop (compute of step i beside the gather of
+    step i-1, double-buffered) with uneven shards: every step's keypoints,
+    offsets and descriptors arrive on rank 0 intact."""
+    procs, q = _spawn(_pipeline_worker)
+    try:
+        ok = q.get(timeout=120)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert [p.exitcode for p in procs] == [0, 0]
+    assert ok
 
 
 def test_gather_keypoints_world2():
@@ -71,6 +155,7 @@ def test_gather_keypoints_world2():
     try:
         ks, offs, ds = q.get(timeout=120)
         shapes = q.get(timeout=120)
+        uneven = q.get(timeout=120)
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -82,3 +167,4 @@ def test_gather_keypoints_world2():
         np.testing.assert_array_equal(offs[r], [0, 2, 5, n])
         assert np.all(ds[r] == r + 1)
     assert shapes == [4, 0]
+    assert uneven == ([4, 5], [[0, 1, 4], [0, 1, 2, 5]])
