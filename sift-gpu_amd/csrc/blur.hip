@@ -114,15 +114,10 @@ __device__ __forceinline__ void blur_tile(const float* __restrict__ src, long lo
       win[4 * q + 2] = t.z;
       win[4 * q + 3] = t.w;
     }
-    // the row's 2w+1 taps in SGPRs up front: one batch of scalar loads and one
-    // wait per kernel row instead of a load + lgkmcnt(0) per tap
     const float* kr = coef + a * T::KS;
-    float kv[T::KS];
-#pragma unroll
-    for (int b = 0; b < T::KS; ++b) kv[b] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(kr[b])));
 #pragma unroll
     for (int b = 0; b < T::KS; ++b) {
-      const float k = kv[b];
+      const float k = kr[b];
       // all kPX products first (distinct registers, pinned by the empty asm),
       // then the kPX adds: no multiply feeds the very next instruction
       float t[kPX];
