@@ -344,16 +344,33 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       const int4 pa = reinterpret_cast<const int4*>(reci + g * 8)[0];
       const int4 pb = reinterpret_cast<const int4*>(reci + g * 8)[1];
       const int pks[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+      // The 8 read-modify-writes are not a chain of LDS round trips: all 8
+      // bins are read at once, a record whose bin an earlier record of this
+      // batch also hit starts from that record's sum (resolved in registers,
+      // so every bin still sees its terms in sample order), and the 8 sums are
+      // written back in order (an aliased bin ends with its last sum).
+      float e[8], h[8], upd[8];
+      int a[8];
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
-        const float e = recv[jj * kRecV + lane];
+        e[jj] = recv[jj * kRecV + lane];
         const int pk = pks[jj];
         const int Rm = (pk & 7) - 1, Cm = ((pk >> 3) & 7) - 1, O0 = pk >> 6;
         const int R = Rm + (qb2 ^ (Rm & 1)), C = Cm + (qb1 ^ (Cm & 1)), O = O0 + (qb0 ^ (O0 & 1));
         const int qidx = ((unsigned)R < 4u && (unsigned)C < 4u) ? (R >> 1) * 10 + (C >> 1) * 5 + (O >> 1) : kTrash;
-        const int a = (qidx << 6) + lane;
-        hist[a] = hist[a] + e;
+        a[jj] = (qidx << 6) + lane;
       }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) h[jj] = hist[a[jj]];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        float b0 = h[jj];
+#pragma unroll
+        for (int kk = 0; kk < jj; ++kk) b0 = a[kk] == a[jj] ? upd[kk] : b0;
+        upd[jj] = b0 + e[jj];
+      }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) hist[a[jj]] = upd[jj];
       wave_sync_d();
       advance();
       vc[0] = vn[0];

@@ -3,7 +3,11 @@ perspectiveTransform (src/main.cpp:44-62), host code in libsift_hip.so
 (homography.hip) behind sift_find_homography / sift_perspective_transform.
 
 OpenCV is not in this image, so parity with its RANSAC (RNG stream, Jacobi,
-LMSolver) is unpinned.  The CPU tests check what the application relies on:
+LMSolver) is unpinned.  The library is pinned value for value against an
+independent numpy restatement of the same algorithm (oracle/homography.py:
+cv::RNG stream, subset checks, normalised DLT, float reprojection test,
+refit + LM), on noisy data with outliers.  The CPU tests also check what the
+application relies on:
 the model is recovered from correspondences with outliers (exactly without
 noise), the inlier mask is the true one, degenerate input gives OpenCV's empty
 result, the run is deterministic, and perspectiveTransform equals its double
@@ -70,6 +74,45 @@ def test_degenerate_inputs(siftgpu):
     H, m = siftgpu.findHomography(sq, sq * 2 + 5)
     np.testing.assert_allclose(H, [[2, 0, 5], [0, 2, 5], [0, 0, 1]], atol=1e-9)
     assert m.all()
+
+
+@pytest.mark.parametrize("seed,n,out_frac,noise", [(10, 60, 0.3, 0.5), (11, 150, 0.5, 1.0), (12, 40, 0.1, 0.0),
+                                                    (13, 200, 0.6, 2.0), (14, 5, 0.0, 0.3)])
+def test_matches_oracle_bitexact(siftgpu, seed, n, out_frac, noise):
+    """sift_find_homography == oracle/homography.py: every H entry (float64
+    bits) and the inlier mask."""
+    import homography as HO  # oracle/ (the checker)
+    rng = np.random.default_rng(seed)
+    src, dst, _ = _data(rng, n, out_frac, noise=noise)
+    H, mask = siftgpu.findHomography(src, dst, siftgpu.RANSAC)
+    Hr, mr = HO.find_homography(src, dst)
+    assert H is not None and Hr is not None
+    assert H.reshape(9).tobytes() == np.array(Hr, np.float64).tobytes(), (H.reshape(9), Hr)
+    assert mask.tobytes() == mr.tobytes()
+    corners = np.array([[0, 0], [640, 0], [640, 480], [0, 480]], np.float32)
+    assert siftgpu.perspectiveTransform(corners, H).tobytes() == HO.perspective_transform(Hr, corners).tobytes()
+
+
+def test_oracle_degenerate_like_library(siftgpu):
+    import homography as HO
+    line = np.c_[np.arange(10), 2 * np.arange(10)].astype(np.float32)
+    assert HO.find_homography(line, line)[0] is None and siftgpu.findHomography(line, line)[0] is None
+    sq = np.array([[0, 0], [10, 0], [10, 10], [0, 10]], np.float32)
+    H, _ = siftgpu.findHomography(sq, sq * 2 + 5)
+    assert H.reshape(9).tobytes() == np.array(HO.find_homography(sq, sq * 2 + 5)[0], np.float64).tobytes()
+
+
+def test_rng_stream():
+    """cv::RNG((uint64)-1): the multiply-with-carry recurrence, restated."""
+    import homography as HO
+    r = HO.RNG()
+    first = [r.next() for _ in range(4)]
+    st = (1 << 64) - 1
+    ref = []
+    for _ in range(4):
+        st = ((st & 0xffffffff) * 4164903690 + (st >> 32)) & ((1 << 64) - 1)
+        ref.append(st & 0xffffffff)
+    assert first == ref
 
 
 def test_perspective_transform_formula(siftgpu):
