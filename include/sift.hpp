@@ -19,19 +19,39 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <sys/time.h>  // the reference header's own includes (include/sift.hpp:11-26)
 
+#include <iostream>
 #include <vector>
 
 #if defined(__has_include)
 #if __has_include(<opencv2/core.hpp>) && !defined(SIFT_HIP_NO_OPENCV)
 #define SIFT_HIP_HAVE_OPENCV 1
 #endif
+#if __has_include(<omp.h>)
+#include <omp.h>
+#endif
 #endif
 
 #ifdef SIFT_HIP_HAVE_OPENCV
+// The reference's OpenCV include set (include/sift.hpp:14-23) minus cuda.h, so
+// a caller like src/main.cpp (imread, imshow, findHomography, cvPoint, ...)
+// compiles against this header unchanged.
 #include <opencv2/core.hpp>
+#include <opencv2/core/hal/hal.hpp>
+#include <opencv2/core/types_c.h>
+#include <opencv2/core/utility.hpp>
 #include <opencv2/features2d.hpp>
 #include <opencv2/imgproc.hpp>
+#if __has_include(<opencv2/imgcodecs.hpp>)
+#include <opencv2/imgcodecs.hpp>
+#endif
+#if __has_include(<opencv2/highgui.hpp>)
+#include <opencv2/highgui.hpp>
+#endif
+#if __has_include(<opencv2/calib3d/calib3d.hpp>)
+#include <opencv2/calib3d/calib3d.hpp>
+#endif
 #if __has_include(<opencv2/xfeatures2d.hpp>)
 #include <opencv2/xfeatures2d.hpp>
 #else

@@ -40,7 +40,7 @@ constexpr int kChunk = 64;         // keypoints ranked together by window radius
 constexpr int kQBins = 21;         // bins per parity class: 2 x 2 x 5 interior + 1 trash
 constexpr int kTrash = 20;         // qidx of the discarded border bins
 constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
-constexpr int kRecV = 68;          // floats per sample row of the owner values (64 + pad)
+constexpr int kRecStride2 = 132;   // words per sample row of the owner records (128 + pad)
 
 struct DescArgs {
   Layout L;
@@ -74,13 +74,12 @@ __device__ __forceinline__ void slab(float a, float b, int& lo, int& hi) {
 
 __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
-  // per-sample hand-off: values [sample p][group*8 + owner slot] (row stride
-  // kRecV floats, == 4 mod 32: the b128 stores of a keypoint group hit distinct
-  // banks) and one packed base-bin word per sample [group*8 + p]
-  __shared__ __attribute__((aligned(16))) float recv[8 * kRecV];
-  __shared__ __attribute__((aligned(16))) int reci[64];
+  // per-sample hand-off records: [sample j][group][owner q] = (bin qidx, value),
+  // row stride kRecStride2 words
+  __shared__ __attribute__((aligned(16))) float rec[8 * kRecStride2];
   __shared__ int rows_tab[kGrp][kMaxWinRows];       // per row: (jlo + 64) | len << 16
   __shared__ float bc[kGrp][4];
+  __shared__ float etab[64];
   __shared__ int sord[kGrp];                        // this sub-batch's keypoint indices
   const int lane = threadIdx.x & 63;
   const int g = lane >> 3, q = lane & 7;
@@ -88,9 +87,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   int n = A.img_kp_off[A.batch];
   if (n > A.kp_cap) n = A.kp_cap;
   const ExpConsts ek = A.mc->e;
-  // exp32f table: lane j holds entry j; looked up with ds_bpermute (no bank
-  // conflicts, unlike a gathered LDS table read)
-  const float etab_v = A.mc->exptab[lane];
+  etab[lane] = A.mc->exptab[lane];
 
   // XCD-aware split (speed only): blocks b and b+8 share an XCD, so XCD x takes
   // one contiguous eighth of the raster-ordered keypoints and its L2 sees the
@@ -218,20 +215,16 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
     // branch-free: an invalid sample hands every owner "+0.0f into your bin 0"
     // (exact no-op, every bin is >= +0) and gathers from a clamped address.
     //
-    // Exchange (the kernel is LDS-cycle bound, VALU has slack): with
+    // The sample's lane resolves ownership for all 8 owners: with
     // (Rm, Cm, O0) = (r0, c0, o0) (interior coordinates, R' = R - 1) and odd =
     // their parity bits, corner k = dr*4 + dc*2 + do lands in interior bin
-    // (Rm+dr, Cm+dc, O0+do), whose parity -- its owner -- is k ^ odd.  The
-    // producer permutes its 8 corner values into owner order in registers
-    // (w[s] = v[s ^ odd], three conditional-swap layers) and stores them with
-    // two ds_write_b128, plus one packed word (Rm, Cm, O0) per sample; each
-    // owner reads its value (ds_read_b32, conflict-free) and the group's 8
-    // packed words (two broadcast ds_read_b128) and derives its bin index
-    //   qidx = (R'>>1)*10 + (C'>>1)*5 + (O>>1), or the trash row when R' or C'
-    // leaves [0, 4).  16 B of records per sample cross LDS instead of 64.
-    float4 vc[2];  // this lane's sample: 8 corner values in owner order
-    int pk_cur = 0;  // packed (Rm+1) | (Cm+1) << 3 | O0 << 6
-    auto sample = [&](bool in_range, float4 (&out)[2], int& pk_out) {
+    // (Rm+dr, Cm+dc, O0+do), whose parity -- its owner -- is k ^ odd, at
+    //   qidx_k = qi0 + [dr and Rm odd]*10 + [dc and Cm odd]*5 + [do and O0 odd],
+    // or in the trash row when Rm+dr or Cm+dc leaves [0, 4).
+    // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
+    // the owner adds its lane to form the [qidx][lane] address.
+    float4 rc_cur[4];  // (qidx, val) x 8 corners of this lane's sample
+    auto sample = [&](bool in_range, float4 (&out)[4], int& odd_out) {
       const int i = ri - radius, j = rlo + u;
       const float c_rot = j * cos_t - i * sin_t;
       const float r_rot = j * sin_t + i * cos_t;
@@ -244,7 +237,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       const float2 mo_raw = gimg[(long long)rcl * pitch + ccl];  // (Mag, Ori) of the pixel
       // invalid: (0, 0) -- border gradients are never written and may hold NaN
       const float2 mo = ok ? mo_raw : make_float2(0.f, 0.f);
-      const float w = exp32f_v((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_v, ek);
+      const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab, ek);
       float obin = (mo.y - ori) * bins_per_rad;
       const float mag = mo.x * w;
       int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
@@ -268,37 +261,22 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       v[0] = v_rc00 - v[1];
       // interior coordinates of the base corner: Rm = R0 - 1 = r0 in [-1, 3]
       const int Rm = ok ? r0 : 0, Cm = ok ? c0 : 0, O0 = ok ? o0 : 0;
-      // owner order: slot s holds corner s ^ odd (odd = parity bits of the base)
-      if (O0 & 1) {
+      const int odd = ((Rm & 1) << 2) | ((Cm & 1) << 1) | (O0 & 1);
+      // corner k's bin index qidx_k (independent of the owner); the store
+      // places it in owner slot k ^ odd, so no value permutation here
+      const int qi0 = (Rm >> 1) * 10 + (Cm >> 1) * 5 + (O0 >> 1);
+      const int a10 = (Rm & 1) ? 10 : 0, a5 = (Cm & 1) ? 5 : 0, a1 = O0 & 1;
+      const bool r0v = Rm >= 0, r1v = Rm <= 2, c0v = Cm >= 0, c1v = Cm <= 2;
+      const int q1 = qi0 + a1, q2 = qi0 + a5, q4 = qi0 + a10;
+      const int qk[8] = {r0v && c0v ? qi0 : kTrash,      r0v && c0v ? q1 : kTrash,
+                         r0v && c1v ? q2 : kTrash,       r0v && c1v ? q2 + a1 : kTrash,
+                         r1v && c0v ? q4 : kTrash,       r1v && c0v ? q4 + a1 : kTrash,
+                         r1v && c1v ? q4 + a5 : kTrash,  r1v && c1v ? q4 + a5 + a1 : kTrash};
 #pragma unroll
-        for (int t = 0; t < 8; t += 2) {
-          const float x = v[t];
-          v[t] = v[t + 1];
-          v[t + 1] = x;
-        }
-      }
-      if (Cm & 1) {
-#pragma unroll
-        for (int t = 0; t < 8; t += 4) {
-          float x = v[t];
-          v[t] = v[t + 2];
-          v[t + 2] = x;
-          x = v[t + 1];
-          v[t + 1] = v[t + 3];
-          v[t + 3] = x;
-        }
-      }
-      if (Rm & 1) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const float x = v[t];
-          v[t] = v[t + 4];
-          v[t + 4] = x;
-        }
-      }
-      out[0] = make_float4(v[0], v[1], v[2], v[3]);
-      out[1] = make_float4(v[4], v[5], v[6], v[7]);
-      pk_out = (Rm + 1) | ((Cm + 1) << 3) | (O0 << 6);
+      for (int t = 0; t < 4; ++t)
+        out[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
+                             v[2 * t + 1]);
+      odd_out = odd;
     };
     // Entry ri+1 of the row table rides in a register (loaded one advance
     // ahead), so the common advance -- at most one row change -- is
@@ -326,56 +304,34 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       }
       enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
     };
+    int odd_cur = 0;
     if (nmax > 0) {
-      sample(q < nsamp, vc, pk_cur);
+      sample(q < nsamp, rc_cur, odd_cur);
       advance();
     }
-    const int qb2 = (q >> 2) & 1, qb1 = (q >> 1) & 1, qb0 = q & 1;
     for (int base = 0; base < nmax; base += 8) {
-      float4* dv4 = reinterpret_cast<float4*>(recv + q * kRecV + g * 8);
-      dv4[0] = vc[0];
-      dv4[1] = vc[1];
-      reci[g * 8 + q] = pk_cur;
+      float2* dst2 = reinterpret_cast<float2*>(rec + q * kRecStride2 + g * 16);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dst2[(2 * t) ^ odd_cur] = make_float2(rc_cur[t].x, rc_cur[t].y);
+        dst2[(2 * t + 1) ^ odd_cur] = make_float2(rc_cur[t].z, rc_cur[t].w);
+      }
       wave_sync_d();
-      float4 vn[2];
-      int pk_nxt = 0;
-      sample(base + 8 + q < nsamp, vn, pk_nxt);
-      // ordered accumulation of batch k: lane q applies its corner of each sample
-      const int4 pa = reinterpret_cast<const int4*>(reci + g * 8)[0];
-      const int4 pb = reinterpret_cast<const int4*>(reci + g * 8)[1];
-      const int pks[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-      // The 8 read-modify-writes are not a chain of LDS round trips: all 8
-      // bins are read at once, a record whose bin an earlier record of this
-      // batch also hit starts from that record's sum (resolved in registers,
-      // so every bin still sees its terms in sample order), and the 8 sums are
-      // written back in order (an aliased bin ends with its last sum).
-      float e[8], h[8], upd[8];
-      int a[8];
+      float4 rc_nxt[4];
+      int odd_nxt = 0;
+      sample(base + 8 + q < nsamp, rc_nxt, odd_nxt);
+      // ordered accumulation of batch k: lane q applies its record of each sample
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
-        e[jj] = recv[jj * kRecV + lane];
-        const int pk = pks[jj];
-        const int Rm = (pk & 7) - 1, Cm = ((pk >> 3) & 7) - 1, O0 = pk >> 6;
-        const int R = Rm + (qb2 ^ (Rm & 1)), C = Cm + (qb1 ^ (Cm & 1)), O = O0 + (qb0 ^ (O0 & 1));
-        const int qidx = ((unsigned)R < 4u && (unsigned)C < 4u) ? (R >> 1) * 10 + (C >> 1) * 5 + (O >> 1) : kTrash;
-        a[jj] = (qidx << 6) + lane;
+        const float2 e = reinterpret_cast<const float2*>(rec + jj * kRecStride2)[lane];
+        const int a = (__float_as_int(e.x) << 6) + lane;
+        hist[a] = hist[a] + e.y;
       }
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) h[jj] = hist[a[jj]];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        float b0 = h[jj];
-#pragma unroll
-        for (int kk = 0; kk < jj; ++kk) b0 = a[kk] == a[jj] ? upd[kk] : b0;
-        upd[jj] = b0 + e[jj];
-      }
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) hist[a[jj]] = upd[jj];
       wave_sync_d();
       advance();
-      vc[0] = vn[0];
-      vc[1] = vn[1];
-      pk_cur = pk_nxt;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) rc_cur[t] = rc_nxt[t];
+      odd_cur = odd_nxt;
     }
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
     float cell[2][8];

@@ -61,6 +61,22 @@ def test_reference_style_caller_compiles(tmp_path, siftgpu):
     assert exe.exists()
 
 
+@pytest.mark.parametrize("openmp", [False, True])
+def test_main_shaped_caller_compiles_with_header_only(tmp_path, siftgpu, openmp):
+    """A src/main.cpp-shaped caller that includes only sift.hpp and uses
+    std::cout, gettimeofday and omp_get_max_threads through it (the reference
+    header's transitive includes, include/sift.hpp:11-26) compiles and links
+    in compat mode (no OpenCV)."""
+    src = os.path.join(ROOT, "tests", "cpp", "main_shape.cpp")
+    exe = tmp_path / "main_shape"
+    cmd = ["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-o", str(exe),
+           "-L", os.path.join(PKG, "lib"), "-lsift_shim", "-lsift_hip", f"-Wl,-rpath,{os.path.join(PKG, 'lib')}"]
+    if openmp:
+        cmd.insert(1, "-fopenmp")
+    subprocess.run(cmd, check=True)
+    assert exe.exists()
+
+
 def test_ctx_create_fails_cleanly_without_gpu(siftgpu):
     import torch
     if torch.cuda.device_count() > 0:

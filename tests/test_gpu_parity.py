@@ -302,3 +302,19 @@ def test_cpp_shim_book(tmp_path, siftgpu, mode):
     db = np.frombuffer(raw[4 + 28 * n:], np.float32).reshape(n, 128)
     assert_bits_equal(kb, g["kps"], "shim keypoints")
     assert_bits_equal(db, g["desc"], "shim descriptors")
+
+
+def test_cpp_main_shaped_caller_runs(tmp_path, siftgpu, oracle):
+    """tests/cpp/main_shape.cpp (includes only sift.hpp, like src/main.cpp)
+    runs SIFT_NCL on the GPU through the shim; its keypoint count equals the
+    CPU path's on the same synthetic pattern."""
+    exe = tmp_path / "main_shape"
+    lib = os.path.join(PKG, "lib")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-fopenmp", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "main_shape.cpp"), "-o", str(exe), "-L", lib,
+                    "-lsift_shim", "-lsift_hip", f"-Wl,-rpath,{lib}"], check=True)
+    out = subprocess.run([str(exe), "200", "240"], check=True, timeout=300, capture_output=True, text=True).stdout
+    i, j = np.meshgrid(np.arange(200), np.arange(240), indexing="ij")
+    img = ((i * 7 + j * 13) % 251).astype(np.float32)
+    n_ref = len(oracle.sift(img)[0])
+    assert f"{n_ref} keypoints, {n_ref} x 128 descriptors" in out, (out, n_ref)
