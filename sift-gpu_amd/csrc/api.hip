@@ -5,9 +5,12 @@
 #include <float.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -39,6 +42,30 @@ Layout make_layout(int rows, int cols, int n_oct) {
   L.g_img = g;
   L.d_img = d;
   return L;
+}
+
+int resident_grid(const void* kernel, int block, size_t lds, int fixed_grid) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  static const bool fixed = [] {
+    const char* e = getenv("SIFT_HIP_FIXED_GRID");
+    return e && atoi(e) != 0;
+  }();
+  if (fixed) return fixed_grid;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fixed_grid;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(kernel, dev);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 ||
+      cus < 1)
+    return fixed_grid;
+  const int g = std::max(8, per_cu * cus / 8 * 8);
+  cache[key] = g;
+  return g;
 }
 
 void host_math_consts(MathConsts* mc) {

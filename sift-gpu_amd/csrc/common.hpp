@@ -173,6 +173,16 @@ struct MathConsts {
 
 void host_math_consts(MathConsts* mc);
 
+// ---- persistent-grid sizing ------------------------------------------------
+// The work-loop kernels (refinement, orientation, descriptors) split their
+// items evenly over the grid.  A grid larger than what the device holds at
+// once runs in rounds, and the last, partial round idles the rest of the chip
+// (8192 orientation waves on 6144 wave slots = 2 rounds for 1.33 rounds of
+// work).  So the grid is the resident count: occupancy API x CUs, a multiple
+// of 8 (the kernels' XCD split), cached per kernel.  SIFT_HIP_FIXED_GRID=1
+// restores the fixed grid (A/B runs).
+int resident_grid(const void* kernel, int block, size_t lds, int fixed_grid);
+
 // ---- host launchers (defined in the .hip files) --------------------------
 struct Plane {          // a device plane (or the input image)
   const float* p;

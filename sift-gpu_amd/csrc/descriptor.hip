@@ -438,7 +438,8 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
   A.desc = desc;
   A.first_octave = first_octave;
   A.err_flag = err_flag;
-  hipLaunchKernelGGL(descriptor_kernel, dim3(8192), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(descriptor_kernel, dim3(resident_grid((const void*)descriptor_kernel, 64, 0, 8192)), dim3(64), 0,
+                     st, A);
 }
 
 }  // namespace sift

@@ -833,8 +833,8 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.couts = D.couts;
   A.npeaks = D.npeaks;
   (void)batch;
-  hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, st, A);
-  hipLaunchKernelGGL(orient_kernel, dim3(8192), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(refine_kernel, dim3(resident_grid((const void*)refine_kernel, 256, 0, 2048)), dim3(256), 0, st, A);
+  hipLaunchKernelGGL(orient_kernel, dim3(resident_grid((const void*)orient_kernel, 64, 0, 8192)), dim3(64), 0, st, A);
 }
 
 // ---- ordered keypoint emission ------------------------------------------------
