@@ -26,7 +26,6 @@
 
 #include <float.h>
 #include <limits.h>
-#include <stdlib.h>
 
 namespace sift {
 
@@ -656,15 +655,8 @@ __device__ __forceinline__ int ori_radius(float size, int o) {
   return cv_round(3 * 1.5f * scl);
 }
 
-// Two accumulation schemes, same bits: ATOMIC -- lane q of each group adds its
-// sample with ds_add_f32 at step q (8 LDS float atomics per batch, ~30 LDS
-// cycles each); otherwise (default) -- each lane owns the bins q, q+8, ...
-// in registers and walks the group's records in sample order, adding the
-// ones that land in its bins (VALU selects instead of LDS atomics).
-template <bool ATOMIC>
 __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
   __shared__ float oh[kOGrp][kOriBins + 4];
-  __shared__ __attribute__((aligned(16))) float2 orec[kOU][64];  // (bin, value) per lane and batch
   __shared__ float sm[kOGrp][kOriBins + 4];
   __shared__ int sord[kOGrp];
   const int lane = threadIdx.x & 63;
@@ -724,7 +716,6 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
     const int D = 2 * radius + 1;
     const int ns = ok ? D * D : 0;
     for (int t = q; t < kOriBins; t += 8) oh[g][t] = 0.f;
-    float hown[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // owner bins q + 8 tt (register histogram)
     int nmax = ns;
     nmax = max(nmax, __shfl_xor(nmax, 8));
     nmax = max(nmax, __shfl_xor(nmax, 16));
@@ -757,7 +748,6 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
         jv[u] = j;
         mo[u] = gimg[okv[u] ? (long long)y * pitch + x : 0];  // (Mag, Ori) of the pixel
       }
-      float2 rv[kOU];
 #pragma unroll
       for (int u = 0; u < kOU; ++u) {
         const float w = exp32f((ii[u] * ii[u] + jv[u] * jv[u]) * escale, etab, ek);
@@ -765,49 +755,10 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
         if (bin >= kOriBins) bin -= kOriBins;
         if (bin < 0) bin += kOriBins;
         const float val = w * mo[u].x;
-        if (ATOMIC) {
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj)
-            if (q == jj && okv[u]) ohist_add(&oh[g][bin], val);
-        } else {
-          // an invalid sample hands owner 0 "+0.0f into bin 0" (exact no-op)
-          rv[u] = okv[u] ? make_float2(__int_as_float(bin), val) : make_float2(0.f, 0.f);
-        }
+        for (int jj = 0; jj < 8; ++jj)
+          if (q == jj && okv[u]) ohist_add(&oh[g][bin], val);
       }
-      if (!ATOMIC) {
-        // every lane of the group applies the group's 8 * kOU records in sample
-        // order to the bins it owns (q, q + 8, ..., held in registers)
-#pragma unroll
-        for (int u = 0; u < kOU; ++u) orec[u][lane] = rv[u];
-        wave_sync();
-#pragma unroll
-        for (int u = 0; u < kOU; ++u) {
-          const float4* r4 = reinterpret_cast<const float4*>(&orec[u][g * 8]);
-          float rb[16];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float4 t4 = r4[k];
-            rb[4 * k] = t4.x;
-            rb[4 * k + 1] = t4.y;
-            rb[4 * k + 2] = t4.z;
-            rb[4 * k + 3] = t4.w;
-          }
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) {
-            const int bin = __float_as_int(rb[2 * jj]);
-            const float add = (bin & 7) == q ? rb[2 * jj + 1] : 0.f;
-            const int t = bin >> 3;
-#pragma unroll
-            for (int tt = 0; tt < 5; ++tt) hown[tt] = hown[tt] + (t == tt ? add : 0.f);  // + 0.0f: exact no-op
-          }
-        }
-        wave_sync();
-      }
-    }
-    if (!ATOMIC) {
-#pragma unroll
-      for (int tt = 0; tt < 5; ++tt)
-        if (q + 8 * tt < kOriBins) oh[g][q + 8 * tt] = hown[tt];
     }
     wave_sync();
     // smoothing (src/sift.cpp:440-451), max, peaks (src/sift.cpp:524-541)
@@ -883,16 +834,7 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.npeaks = D.npeaks;
   (void)batch;
   hipLaunchKernelGGL(refine_kernel, dim3(resident_grid((const void*)refine_kernel, 256, 0, 2048)), dim3(256), 0, st, A);
-  static const bool atomic_hist = [] {
-    const char* e = getenv("SIFT_HIP_ORIENT_ATOMIC");
-    return e && atoi(e) != 0;
-  }();
-  if (atomic_hist)
-    hipLaunchKernelGGL(orient_kernel<true>, dim3(resident_grid((const void*)orient_kernel<true>, 64, 0, 8192)),
-                       dim3(64), 0, st, A);
-  else
-    hipLaunchKernelGGL(orient_kernel<false>, dim3(resident_grid((const void*)orient_kernel<false>, 64, 0, 8192)),
-                       dim3(64), 0, st, A);
+  hipLaunchKernelGGL(orient_kernel, dim3(resident_grid((const void*)orient_kernel, 64, 0, 8192)), dim3(64), 0, st, A);
 }
 
 // ---- ordered keypoint emission ------------------------------------------------
