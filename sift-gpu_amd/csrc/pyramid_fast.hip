@@ -252,6 +252,7 @@ struct FastArgs {
   int pitch, rows, cols;
   int srows, scols;        // source (previous octave) shape
   int chunk;               // rows per workgroup (multiple of kRB)
+  int ify2;                // octave > 0 and srows == 2 * rows: ify is exactly 2
   FastCoefs coef;          // by value: scalar loads from the argument segment
 };
 
@@ -365,7 +366,9 @@ __device__ __forceinline__ void fetch_decim(const FastArgs& A, const float* __re
     const int y = Z + r;
     const int sx = xmap[i < kRB * kBW ? c : 0];
     const bool ok = i < kRB * kBW && y >= 0 && y < A.rows && sx >= 0;
-    int sy = (int)floor(max(y, 0) * A.ify);
+    // resize NN row map; exactly 2y when the source has twice the rows
+    // (ify == 2.0 then, and floor(2y) needs no double arithmetic)
+    int sy = A.ify2 ? 2 * max(y, 0) : (int)floor(max(y, 0) * A.ify);
     sy = sy < A.srows - 1 ? sy : A.srows - 1;
     P.g[u] = ld1_async(prev + (ok ? (long long)sy * A.s_pitch + sx : 0));
   }
@@ -686,18 +689,29 @@ void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Pl
     A.scols = P.cols;
     A.ifx = 1. / ((double)O.cols / P.cols);
     A.ify = 1. / ((double)O.rows / P.rows);
+    A.ify2 = P.rows == 2 * O.rows && A.ify == 2.0;
   }
-  // Chunk the rows so the launch has ~1.5k workgroups (2 resident per CU),
-  // but never below 48 rows (the 42-row lead is recomputed per chunk).
+  // Row chunks per strip: every chunk walks kLead + kH = 42 rows it does not
+  // output, and the grid runs in rounds of `resident` workgroups (2 per CU),
+  // so pick the chunk count that minimises rounds x rows walked per chunk
+  // (octave 1 of a 64 x 1080p batch: 1 chunk, not 3; octave 2: 2, not 6).
   const int strips = (O.cols + kFW - 1) / kFW;
   const long long per = (long long)strips * batch;
-  int chunks = (int)((1536 + per - 1) / per);
-  const int max_chunks = (O.rows + 47) / 48;
-  chunks = chunks > max_chunks ? max_chunks : chunks;
-  if (chunks < 1) chunks = 1;
-  int ch = (O.rows + chunks - 1) / chunks;
-  ch = (ch + kRB - 1) / kRB * kRB;
-  chunks = (O.rows + ch - 1) / ch;
+  const int resident = resident_grid(
+      o > 0 ? (const void*)pyr_fast_kernel<false, false> : (const void*)pyr_fast_kernel<true, true>, 256, 0, 512);
+  int ch = 0;
+  double best = 0;
+  for (int c = 1; c <= (O.rows + kRB - 1) / kRB; ++c) {
+    const int h = ((O.rows + c - 1) / c + kRB - 1) / kRB * kRB;
+    const int cc = (O.rows + h - 1) / h;
+    const double rounds = (double)((per * cc + resident - 1) / resident);
+    const double cost = rounds * (h + kLead + kH);
+    if (ch == 0 || cost < best) {
+      best = cost;
+      ch = h;
+    }
+  }
+  const int chunks = (O.rows + ch - 1) / ch;
   A.chunk = ch;
   dim3 grid(strips, chunks, batch);
   if (o > 0)
