@@ -28,6 +28,8 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--tag", default="")
     p.add_argument("--fast", action="store_true", help="SIFT_FLAG_FAST pyramid")
+    p.add_argument("--ignore-status", action="store_true",
+                   help="ablation runs: ignore capacity overflows of garbage planes")
     a = p.parse_args()
     B, R, C = a.batch, a.rows, a.cols
     ctx = siftgpu.Context(R, C, B, flags=siftgpu.SIFT_FLAG_PROFILE | (siftgpu.SIFT_FLAG_FAST if a.fast else 0))
@@ -42,12 +44,19 @@ def main():
         ctx.detect_compute_batch(imgs.data_ptr(), B, R, C, C, R * C, kpts.data_ptr(), desc.data_ptr(), cap,
                                  offs.data_ptr())
 
+    def sync():
+        try:
+            ctx.sync()
+        except siftgpu.SiftError:
+            if not a.ignore_status:
+                raise
+
     run()
-    ctx.sync()
+    sync()
     ctx.stage_stats(reset=True)
     for _ in range(a.reps):
         run()
-    ctx.sync()
+    sync()
     st = ctx.stage_stats(reset=True)
     total = sum(v["ms"] for v in st.values()) / a.reps
     out = {"tag": a.tag, "batch": B, "shape": [R, C], "keypoints": int(offs[-1].item()),
