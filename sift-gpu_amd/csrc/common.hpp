@@ -219,6 +219,10 @@ void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int n
                    float2* part_d, int2* part_i, int* idx, float* dist);
 void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
                          const void* coef);
+// pyramid_fast2.hip: the same planes bit for bit from 64-column strips (4
+// workgroups per CU) and a separate octave-0 base kernel.
+void launch_pyramid_fast2(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
+                          const void* coef);
 
 // detect.hip
 struct DetectBufs {
