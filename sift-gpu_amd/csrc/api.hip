@@ -298,14 +298,6 @@ int alloc_candidates(sift_ctx* c, int cap) {
 
 double plane_px(const Layout& L, int o) { return (double)L.oct[o].rows * L.oct[o].cols; }
 
-// SIFT_HIP_PYR_ONLY=1 (kernel ablation runs only): the batch entry points
-// build the pyramid and stop, so planes computed by an ablated kernel never
-// reach the detection kernels.
-bool ablation_pyramid_only() {
-  static const bool on = getenv("SIFT_HIP_PYR_ONLY") && atoi(getenv("SIFT_HIP_PYR_ONLY"));
-  return on;
-}
-
 // Gaussian pyramid (src/sift.cpp:229-263) + DoG (:265-283) for a batch whose
 // input planes are described by src.  Async on c->stream.
 void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool with_dog) {
@@ -317,11 +309,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       const double px = plane_px(L, o) * batch;
       const double taps = 2.0 * (9 + 17 + 25 + 37) + (o == 0 ? 2.0 * 9 : 0.0);
       StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-      static const bool v1 = getenv("SIFT_HIP_FAST_V1") && atoi(getenv("SIFT_HIP_FAST_V1"));
-      if (v1)
-        launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
-      else
-        launch_pyramid_fast2(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
+      launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
     }
     if (with_dog)
       for (int o = 0; o < L.n_oct; ++o) {
@@ -749,12 +737,11 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
     (void)hipEventRecord(v0, c->stream);
     enqueue_pyramid(c, L, src, batch, false);
     (void)hipEventRecord(v1, c->stream);
-    if (!ablation_pyramid_only())
-      enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
+    enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
     (void)hipEventRecord(v2, c->stream);
-    if (!ablation_pyramid_only()) enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
+    enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
     (void)hipEventRecord(v3, c->stream);
-    if (!ablation_pyramid_only()) enqueue_status(c, true, d_img_offsets, batch, kp_cap);
+    enqueue_status(c, true, d_img_offsets, batch, kp_cap);
     verbose_phase(c, "pyramid construction time", v0, v1);
     verbose_phase(c, "keypoint localization time", v1, v2);
     verbose_phase(c, "descriptor extraction time", v2, v3);
@@ -778,7 +765,6 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
   key_put(key, c->flags);
   return run_graphed(c, key, [&]() {
     enqueue_pyramid(c, L, src, batch, false);
-    if (ablation_pyramid_only()) return;
     enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
     enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
     enqueue_status(c, true, d_img_offsets, batch, kp_cap);

@@ -105,22 +105,6 @@ __device__ __forceinline__ float exp32f(float v, const float* __restrict__ tab,
   return sc * tab[vi & 63] * poly;
 }
 
-// The same with the table held one entry per lane (lane j: tab[j]) and read
-// with a cross-lane permute; every lane of the wave must be active.
-__device__ __forceinline__ float exp32f_v(float v, float tab_lane, const ExpConsts& k) {
-  v = v < k.lo ? k.lo : v;
-  v = k.hi < v ? k.hi : v;
-  v = v * k.prescale;
-  int vi = cv_round(v);
-  v = (v - (float)vi) * k.post;
-  int t = (vi >> 6) + 127;
-  t = !(t & ~255) ? t : t < 0 ? 0 : 255;
-  float sc = __int_as_float(t << 23);
-  float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
-  const float tv = __int_as_float(__builtin_amdgcn_ds_bpermute((vi & 63) << 2, __float_as_int(tab_lane)));
-  return sc * tv * poly;
-}
-
 // hal::fastAtan2 in degrees.
 struct AtanConsts {
   float p1, p3, p5, p7, eps;
@@ -219,10 +203,6 @@ void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int n
                    float2* part_d, int2* part_i, int* idx, float* dist);
 void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
                          const void* coef);
-// pyramid_fast2.hip: the same planes bit for bit from 64-column strips (4
-// workgroups per CU) and a separate octave-0 base kernel.
-void launch_pyramid_fast2(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
-                          const void* coef);
 
 // detect.hip
 struct DetectBufs {

@@ -134,39 +134,3 @@ def test_fast_batch_equals_single(fctx, oracle):
         assert o[b + 1] - o[b] == len(ks)
         assert k[o[b]:o[b + 1]].tobytes() == np.ascontiguousarray(ks).view(np.uint8).tobytes()
         assert dd[o[b]:o[b + 1]].tobytes() == ds.tobytes()
-
-
-_PLANE_DIGESTS = r'''
-import hashlib, json, sys
-sys.path[:0] = sys.argv[1:3]
-import torch  # noqa: F401
-import numpy as np
-import oracle as O
-import siftgpu as S
-c = S.Context(1080, 1920, 4, device=0, flags=0x1)
-out = {}
-for b, (r, w) in enumerate([(1080, 1920), (203, 157), (33, 1200), (300, 210), (130, 90), (517, 1031)]):
-    gp = c.buildGaussianPyramid(O.synth_image(b, r, w), 5)
-    out[f"{r}x{w}"] = hashlib.sha256(b"".join(np.ascontiguousarray(p).tobytes() for p in gp)).hexdigest()
-c.close()
-print(json.dumps(out))
-'''
-
-
-def test_fast_pyramid_strips_equal_wide_strips():
-    """pyramid_fast2.hip (64-column strips, separate octave-0 base kernel, the
-    default) and pyramid_fast.hip (128-column strips, SIFT_HIP_FAST_V1=1) run
-    the same FMA chains in the same tap order: every plane bit-identical."""
-    import json
-    import os
-    import subprocess
-    import sys
-    from conftest import ORACLE_DIR, PKG
-    res = {}
-    for v1 in ("0", "1"):
-        env = dict(os.environ, SIFT_HIP_FAST_V1=v1)
-        p = subprocess.run([sys.executable, "-c", _PLANE_DIGESTS, PKG, ORACLE_DIR], env=env, capture_output=True,
-                           text=True, timeout=300)
-        assert p.returncode == 0, p.stderr[-2000:]
-        res[v1] = json.loads(p.stdout.strip().splitlines()[-1])
-    assert res["0"] == res["1"]

@@ -1,18 +1,11 @@
-"""ISA check for the fast pyramids' untracked prefetch (ld2_async / ld1_async /
-ld1u).
+"""ISA check for pyramid_fast.hip's untracked prefetch (ld2_async / ld1_async).
 
-Compiles the file to gfx950 assembly and, per walking kernel instance, checks
+Compiles the file to gfx950 assembly and, per pyr_fast_kernel instance, checks
 that no instruction touches a prefetch destination register between the
 asm load and the explicit `s_waitcnt vmcnt(N)` that ends the column passes,
 and reports the VMEM stores in between.  Exit status 1 on a violation.
 
-    python tools/check_prefetch_isa.py            # pyramid_fast.hip
-    python tools/check_prefetch_isa.py --v2       # pyramid_fast2.hip
-
-pyramid_fast2.hip feeds its stage with inline-asm LDS DMA (M0 set in the same
-asm statement); --v2 checks instead that nothing else in pyr_scales_kernel
-reads or writes M0 and that no s_barrier is preceded by a vmcnt wait the
-compiler added (the DMA lead and plane stores stay in flight across barriers).
+    python tools/check_prefetch_isa.py
 """
 import os
 import re
@@ -20,9 +13,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-V2 = '--v2' in sys.argv
-SRC = os.path.join(ROOT, 'sift-gpu_amd', 'csrc', 'pyramid_fast2.hip' if V2 else 'pyramid_fast.hip')
-KERNEL = 'pyr_scales_kernel' if V2 else 'pyr_fast_kernel'
+SRC = os.path.join(ROOT, 'sift-gpu_amd', 'csrc', 'pyramid_fast.hip')
 
 
 def regs(tok):
@@ -40,41 +31,17 @@ def all_regs(line):
     return out
 
 
-def check_v2(s):
-    bad = 0
-    for m in re.finditer(r'^(_ZN4sift\S*pyr_scales_kernel\S*):', s, re.M):
-        L = s[m.end():s.index('.Lfunc_end', m.end())].split('\n')
-        for i, l in enumerate(L):
-            t = l.strip()
-            if t.startswith(';') or 'm0' not in t:
-                continue
-            if not (t.startswith('s_mov_b32 m0,') and 'global_load_lds' in ''.join(L[i + 1:i + 3])):
-                print('  M0 use outside the DMA asm:', t)
-                bad += 1
-        for i, l in enumerate(L):
-            if l.strip() == 's_barrier':
-                prev = [x.strip() for x in L[max(0, i - 3):i]]
-                if any(re.match(r's_waitcnt.*vmcnt\((\d+)\)', x) and 'vmcnt(63)' not in x for x in prev):
-                    print('  vmcnt wait before s_barrier at line', i, prev)
-                    bad += 1
-        dma = sum('global_load_lds_dwordx4' in l for l in L)
-        print(f'{m.group(1)}: {dma} DMA sites, {bad} violations')
-    sys.exit(1 if bad else 0)
-
-
 def main():
     asm = '/tmp/pyramid_fast_check.s'
     subprocess.check_call(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '--offload-arch=gfx950', '-ffp-contract=off',
                            '-fno-slp-vectorize', '-I' + os.path.join(ROOT, 'include'), '--cuda-device-only', '-S',
                            SRC, '-o', asm], stderr=subprocess.DEVNULL)
     s = open(asm).read()
-    if V2:
-        check_v2(s)
     bad = 0
-    for m in re.finditer(r'^(_ZN4sift\S*' + KERNEL + r'\S*):', s, re.M):
+    for m in re.finditer(r'^(_ZN4sift\S*pyr_fast_kernel\S*):', s, re.M):
         start = m.end()
         L = s[start:s.index('.Lfunc_end', start)].split('\n')
-        tag = re.search(r'ILb\d(ELb\d)?', m.group(1)).group(0)
+        tag = re.search(r'ILb(\d)ELb(\d)', m.group(1)).group(0)
         waits = [i for i, l in enumerate(L) if re.search(r's_waitcnt vmcnt\(\d+\)', l)]
         loads = [i for i, l in enumerate(L) if re.search(r'global_load_dword', l)]
         n = 0
