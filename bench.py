@@ -45,6 +45,7 @@ import sift_dist  # noqa: E402
 METRIC = "Mpix/s + keypoints/s, 1920×1080 grayscale, 1/2/4/8 MI355X vs CPU ref"
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector peak (FMA = 2 flops, 2-cycle wave64 issue)
 VALU_OP_PEAK_T = 78.65     # non-FMA fp32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+VALU_ISSUE_PEAK_G = 1228.8  # wave64 VALU instructions/s (G): 256 CU x 4 SIMD x 2.4 GHz / 2 cycles
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic.json")
@@ -197,6 +198,30 @@ def traffic_of(tr, kernel):
     if not k:
         return None, None
     return k["read_bytes"] + k["write_bytes"], tr.get("source")
+
+
+def descriptor_roofline(tr, d):
+    """descriptor_kernel against the VALU issue ceiling: its work is integer /
+    float bookkeeping per window sample (gather, exp32f, trilinear weights, bin
+    hand-off), no FMA stream, so the bound is wave-instructions issued.
+    achieved = SQ_INSTS_VALU per launch (committed rocprofv3 SQ pass over
+    tools/stage_bench.py, same 64 x 1080p batch) / the live average launch
+    time; peak = 256 CU x 4 SIMD x 2.4 GHz / 2 cycles per wave64 VALU
+    instruction (MI355X_MICROARCH.md)."""
+    launches = max(d["launches"], 1)
+    ms = d["ms"] / launches
+    k = tr.get("kernels", {}).get("descriptor_kernel", {})
+    valu = k.get("valu_insts")
+    out = {"bound": "valu", "unit": "Ginstr/s", "peak": VALU_ISSUE_PEAK_G, "kernel": "descriptor_kernel",
+           "avg_launch_ms": round(ms, 4), "valu_insts_per_launch": valu, "lds_insts_per_launch": k.get("lds_insts"),
+           "traffic": (k["read_bytes"] + k["write_bytes"]) if "read_bytes" in k else None,
+           "traffic_source": tr.get("source")}
+    if valu and ms:
+        g = valu / (ms * 1e-3) / 1e9
+        out.update({"achieved": round(g, 1), "frac": round(g / VALU_ISSUE_PEAK_G, 4)})
+    else:
+        out.update({"achieved": None, "frac": None})
+    return out
 
 
 # ---- single image (configs[1]) ------------------------------------------------
@@ -462,7 +487,8 @@ def main():
             if d:
                 out["descriptor"] = {"ms_per_step": round(d["ms"] / a.steps, 3),
                                      "keypoints_per_s_kernel": round(kp_total_step / world * a.steps /
-                                                                     (d["ms"] * 1e-3), 1)}
+                                                                     (d["ms"] * 1e-3), 1),
+                                     "roofline": descriptor_roofline(tr, d)}
         if fast is not None:
             fdt, fst, fkp = fast
             mpix = world * B * R * C * a.steps / 1e6

@@ -139,9 +139,17 @@ def main():
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
         json.dump({"bench": bench, "calibration": cal, "kernels": summary, "sq": sq}, f, indent=1)
+    # VALU / LDS wave-instructions per dispatch (SQ pass over tools/stage_bench.py,
+    # the same 64 x 1080p batch): bench.py's VALU-issue rooflines
+    for name, v in sq.items():
+        if name in traffic and "SQ_INSTS_VALU" in v:
+            traffic[name]["valu_insts"] = round(v["SQ_INSTS_VALU"])
+            traffic[name]["lds_insts"] = round(v.get("SQ_INSTS_LDS", 0))
+            traffic[name]["waves"] = round(v.get("SQ_WAVES", 0))
     with open(os.path.join(out, "traffic.json"), "w") as f:
         json.dump({"source": f"profiles/{tag}_summary.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes over "
-                             f"bench.py, calibrated by tools/fetch_calib)", "kernels": traffic}, f, indent=1)
+                             f"bench.py, calibrated by tools/fetch_calib; SQ_INSTS_* from the SQ pass over "
+                             f"tools/stage_bench.py)", "kernels": traffic}, f, indent=1)
     print("\n".join(lines))
 
 
