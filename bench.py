@@ -200,6 +200,15 @@ def traffic_of(tr, kernel):
     return k["read_bytes"] + k["write_bytes"], tr.get("source")
 
 
+def valu_issue_frac(tr, kernel, launch_ms):
+    """SQ_INSTS_VALU per launch (committed PMC pass) / the live launch time,
+    as a fraction of the wave64 VALU issue peak (VALU_ISSUE_PEAK_G)."""
+    valu = tr.get("kernels", {}).get(kernel, {}).get("valu_insts")
+    if not valu or not launch_ms:
+        return None
+    return round(valu / (launch_ms * 1e-3) / 1e9 / VALU_ISSUE_PEAK_G, 4)
+
+
 def descriptor_roofline(tr, d):
     """descriptor_kernel against the VALU issue ceiling: its work is integer /
     float bookkeeping per window sample (gather, exp32f, trilinear weights, bin
@@ -267,6 +276,20 @@ def single_image_leg(R, C, steps, warmup, octaves=4):
             kps, dsc = ctx.SIFT_NCL(host)
             ts.append(time.perf_counter() - t0)
         out["host_ms"] = round(float(np.median(ts)) * 1e3, 4)
+        # H2D / D2H separately: the host call's upload and
+        # download stages, HIP events on the context stream (PROFILE mode)
+        ctx.set_flags(siftgpu.SIFT_FLAG_PROFILE)
+        ctx.stage_stats(reset=True)
+        reps = max(steps, 10)
+        for _ in range(reps):
+            ctx.SIFT_NCL(host)
+        st = ctx.stage_stats(reset=True)
+        ctx.set_flags(0)
+        for k in ("upload", "download"):
+            if k in st and st[k]["ms"] > 0:
+                ms = st[k]["ms"] / reps
+                out[f"{k}_ms"] = round(ms, 4)
+                out[f"{k}_GBs"] = round(st[k]["bytes"] / reps / (ms * 1e-3) / 1e9, 2)
         gb = np.load(os.path.join(GOLDEN, "batch_1080x1920.npz"), allow_pickle=False)
         verified = (R, C) == (1080, 1920) and octaves == 4 and len(kps) == int(gb["oct4_n"]) and \
             _sha(kps) == str(gb["oct4_kp_sha"]) and _sha(dsc) == str(gb["oct4_desc_sha"])
@@ -279,7 +302,9 @@ def single_image_leg(R, C, steps, warmup, octaves=4):
         "keypoints_per_s_host_to_host": round(n / (out["host_ms"] * 1e-3), 1),
         "note": "latency = median wall time of one call + sift_sync, image resident in HBM; host_ms = "
                 "SIFT_NCL from host memory to host memory (H2D 8.3 MB, graphed compute, one wait, D2H of n "
-                "records); output_verified = the host call's keypoints/descriptors equal the CPU path's "
+                "records); upload/download = the H2D image copy and D2H result copy of that call alone "
+                "(pageable host memory, HIP events); output_verified = the host call's keypoints/descriptors "
+                "equal the CPU path's "
                 "(5-octave output filtered to octave <= 3, tests/golden/batch_1080x1920.npz)"})
     return out
 
@@ -443,11 +468,14 @@ def main():
                     "traffic_source": tsrc,
                     "kernel": "blur_octave_kernel",
                     "avg_launch_ms": round(per_launch_ms, 4),
+                    "valu_issue_frac": valu_issue_frac(tr, "blur_octave_kernel", per_launch_ms),
                     "note": "exact-mode 2-D blur is fp32-VALU bound, no MFMA; peak = the fp32 vector peak "
                             "(FMA counted as 2 flops); the parity contract forbids FMA, so each tap is one "
                             "multiply + one add instruction and the ceiling is frac 0.5; flops = 2 x taps per "
                             "launch (one octave, 4 scales, whole batch); traffic = HBM bytes per launch from "
-                            "the committed rocprofv3 PMC pass (calibrated FETCH_SIZE/WRITE_SIZE)"}
+                            "the committed rocprofv3 PMC pass (calibrated FETCH_SIZE/WRITE_SIZE); "
+                            "valu_issue_frac = SQ_INSTS_VALU per launch (same PMC pass) / launch time / the "
+                            "wave64 VALU issue peak (256 CU x 4 SIMD x 2.4 GHz / 2 cycles)"}
             pyr_ms = sum(stats[k]["ms"] for k in ("blur_base", "blur_octave", "decimate", "dog") if k in stats)
             pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
             out.update({

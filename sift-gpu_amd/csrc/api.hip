@@ -714,10 +714,13 @@ int sift_copy_results(sift_ctx* c, sift_keypoint* kpts, float* desc, int cap, in
   if (n == 0) return SIFT_OK;
   if (!kpts || (desc && !c->last_has_desc)) return fail(c, SIFT_E_INVALID, "nothing to copy into");
   (void)hipSetDevice(c->device);
-  HIP_TRY(c, hipMemcpyAsync(kpts, c->d_kpts, sizeof(sift_keypoint) * n, hipMemcpyDeviceToHost, c->stream));
-  if (desc)
-    HIP_TRY(c, hipMemcpyAsync(desc, c->d_desc, sizeof(float) * kDescLen * n, hipMemcpyDeviceToHost,
-                              c->stream));
+  {
+    StageScope s(c, ST_DOWNLOAD, 0, (28.0 + (desc ? 512.0 : 0.0)) * n);
+    HIP_TRY(c, hipMemcpyAsync(kpts, c->d_kpts, sizeof(sift_keypoint) * n, hipMemcpyDeviceToHost, c->stream));
+    if (desc)
+      HIP_TRY(c, hipMemcpyAsync(desc, c->d_desc, sizeof(float) * kDescLen * n, hipMemcpyDeviceToHost,
+                                c->stream));
+  }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return SIFT_OK;
 }
