@@ -8,9 +8,14 @@ extrema + refinement + orientation, 128-D descriptors -- over one batch of
 BASELINE.json configs[2] at N=1; at N=8 the 8 x 64 = 512 images are
 configs[3]).  Inputs are generated on device (integer-exact generator,
 SURVEY.md 8(d) d2) before the timed region; every rank has its own images
-(weak scaling).  For N > 1 each step's keypoints are gathered to rank 0 over
-RCCL one step behind the compute (sift-gpu_amd/sift_dist.py), and the last
-step's gather is inside the timed region.
+(weak scaling).  The timed step runs the per-GPU batch as --streams (default
+4) sub-batches, one library context and HIP stream each, with no
+synchronisation between them inside the timed region (graph replay; the
+streams' stages overlap).  For N > 1 each sub-batch's keypoints are gathered
+to rank 0 over RCCL one step behind the compute (sift-gpu_amd/sift_dist.py),
+and the last step's gather is inside the timed region.  Stage times and the
+per-kernel rooflines come from a separate serial leg (one context, the whole
+batch, HIP events around every stage).
 
 Outside the timed region rank 0 checks its image 0 (seed 0) -- and seeds 31
 and 63 at the default shape -- against the CPU path's SHA-256 digests
@@ -65,6 +70,8 @@ def parse():
     p.add_argument("--no-fast", action="store_true", help="skip the SIFT_FLAG_FAST leg")
     p.add_argument("--no-match", action="store_true", help="skip the knnMatch leg (SURVEY 8(f) f2)")
     p.add_argument("--no-single", action="store_true", help="skip the configs[1] single-image leg")
+    p.add_argument("--streams", type=int, default=4,
+                   help="timed legs: the per-GPU batch as this many sub-batches, one context + HIP stream each")
     p.add_argument("--only", default=None, choices=[None, "exact", "fast", "single"],
                    help="profiling runs: time only this leg")
     p.add_argument("--profile-json", default=None, help="also write per-stage stats here")
@@ -158,9 +165,10 @@ def _sha(a) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def verify_outputs(kpts, desc, offs, R, C, B, octaves, seed_base):
+def verify_outputs(parts, R, C, octaves, seed_base):
     """Digest check of this rank's outputs against the CPU path's
-    (tests/golden/make_golden.py).  Returns (verified seeds, failures)."""
+    (tests/golden/make_golden.py).  parts: (first image, images, kpts, desc,
+    offs) per sub-batch.  Returns (verified seeds, failures)."""
     if octaves != 5 or (R, C) != (1080, 1920):
         return [], ["no golden digests for this shape / octave count"]
     gold = {}
@@ -169,19 +177,20 @@ def verify_outputs(kpts, desc, offs, R, C, B, octaves, seed_base):
     gb = np.load(os.path.join(GOLDEN, "batch_1080x1920.npz"), allow_pickle=False)
     for s, n, ks, ds in zip(gb["seeds"], gb["n"], gb["kp_sha"], gb["desc_sha"]):
         gold[int(s)] = (int(n), str(ks), str(ds))
-    o = offs.cpu().numpy().astype(np.int64)
     ok, bad = [], []
     for seed, (n, ks, ds) in sorted(gold.items()):
-        b = seed - seed_base
-        if not 0 <= b < B:
-            continue
-        a, e = int(o[b]), int(o[b + 1])
-        k = kpts[a:e].cpu().numpy()
-        d = desc[a:e].cpu().numpy()
-        if e - a == n and _sha(k) == ks and _sha(d) == ds:
-            ok.append(seed)
-        else:
-            bad.append(seed)
+        for b0, nb, kpts, desc, offs in parts:
+            b = seed - seed_base - b0
+            if not 0 <= b < nb:
+                continue
+            o = offs.cpu().numpy().astype(np.int64)
+            a, e = int(o[b]), int(o[b + 1])
+            k = kpts[a:e].cpu().numpy()
+            d = desc[a:e].cpu().numpy()
+            if e - a == n and _sha(k) == ks and _sha(d) == ds:
+                ok.append(seed)
+            else:
+                bad.append(seed)
     return ok, bad
 
 
@@ -376,63 +385,98 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
     B, R, C = a.batch, a.rows, a.cols
-    stream = torch.cuda.current_stream()
-    ctx = siftgpu.Context(R, C, B, device=dev, flags=siftgpu.SIFT_FLAG_PROFILE)
-    ctx.set_stream(stream.cuda_stream)
-    ctx.set_octaves(a.octaves)
+    S = max(1, min(a.streams, B // 2))
     seed_base = rank * B
-
     imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
-    ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=seed_base)
-    cap = B * 40000
     gathering = world > 1 and not a.no_gather
-    nslots = 2 if gathering else 1
-    bufs = [(torch.empty((cap, 7), dtype=torch.int32, device="cuda"),
-             torch.empty((cap, 128), dtype=torch.float32, device="cuda"),
-             torch.empty((B + 1,), dtype=torch.int32, device="cuda")) for _ in range(nslots)]
-    runner = None
     gathered = {"steps": 0, "keypoints": 0}
-    if gathering:
-        def on_result(step, out):
-            gathered["steps"] += 1
-            gathered["keypoints"] += sum(int(o[-1]) for o in out[1])
-        pipe = sift_dist.GatherPipeline(sift_dist.shard_sizes(world * B, world), cap, dst=0)
-        runner = sift_dist.PipelinedSteps(pipe, bufs, with_desc=False, on_result=on_result)
 
-    def compute(k, d, o):
-        ctx.detect_compute_batch(imgs.data_ptr(), B, R, C, C, R * C, k.data_ptr(), d.data_ptr(), cap, o.data_ptr())
+    class Part:
+        """One context on one stream over images [b0, b0 + nb) of this rank's
+        batch; with `gather`, its results go to rank 0 one step behind
+        (sift_dist.PipelinedSteps, two result slots)."""
 
-    def step():
-        if runner is not None:
-            runner.step(compute)
-        else:
-            compute(*bufs[0])
+        def __init__(self, b0, nb, strm, gather):
+            self.b0, self.nb, self.stream = b0, nb, strm
+            self.ctx = siftgpu.Context(R, C, nb, device=dev)
+            self.ctx.set_stream(strm.cuda_stream)
+            self.ctx.set_octaves(a.octaves)
+            self.cap = nb * 40000
+            self.bufs = [(torch.empty((self.cap, 7), dtype=torch.int32, device="cuda"),
+                          torch.empty((self.cap, 128), dtype=torch.float32, device="cuda"),
+                          torch.empty((nb + 1,), dtype=torch.int32, device="cuda")) for _ in range(2 if gather else 1)]
+            self.runner = None
+            if gather:
+                def on_result(step, out, first=(b0 == 0)):
+                    gathered["steps"] += 1 if first else 0
+                    gathered["keypoints"] += sum(int(o[-1]) for o in out[1])
+                pipe = sift_dist.GatherPipeline([nb] * world, self.cap, dst=0)
+                self.runner = sift_dist.PipelinedSteps(pipe, self.bufs, with_desc=False, on_result=on_result)
 
-    def leg(flags):
-        """W warmup + K timed steps in one mode; returns (max-over-ranks seconds,
-        per-stage device stats of this rank, keypoints per step summed over ranks)."""
-        ctx.set_flags(flags)
+        def compute(self, k, d, o):
+            self.ctx.detect_compute_batch(imgs[self.b0].data_ptr(), self.nb, R, C, C, R * C, k.data_ptr(),
+                                          d.data_ptr(), self.cap, o.data_ptr())
+
+        def step(self):
+            with torch.cuda.stream(self.stream):
+                if self.runner is not None:
+                    self.runner.step(self.compute)
+                else:
+                    self.compute(*self.bufs[0])
+
+        def flush(self):
+            if self.runner is not None:
+                with torch.cuda.stream(self.stream):
+                    self.runner.flush()
+
+        def close(self):
+            self.ctx.close()
+
+    # The timed step: the batch as S sub-batches, one context and HIP stream
+    # each, no synchronisation between them inside the timed region -- the
+    # streams drift out of phase, so one's descriptor phase runs beside
+    # another's blur (DESIGN.md 6-7).  Per-kernel rooflines and stage times
+    # come from a separate serial leg: one context, the whole batch, HIP events
+    # around every stage (concurrent kernels would inflate each other's times).
+    parts = [Part(B * s // S, B * (s + 1) // S - B * s // S,
+                  torch.cuda.Stream() if S > 1 else torch.cuda.current_stream(), gathering) for s in range(S)]
+    serial = Part(0, B, torch.cuda.current_stream(), False)
+    serial.ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=seed_base)
+    torch.cuda.synchronize()
+
+    def leg(ps, flags):
+        """W warmup + K timed steps of parts ps in one mode; returns (max-over-
+        ranks seconds, per-stage device stats of this rank (one part), keypoints
+        per step summed over ranks)."""
+        for p in ps:
+            p.ctx.set_flags(flags)
         for _ in range(a.warmup):
-            step()
-        if runner is not None:
-            runner.flush()
-        ctx.sync()  # sticky device status: candidate / keypoint capacity
-        ctx.stage_stats(reset=True)
+            for p in ps:
+                p.step()
+        for p in ps:
+            p.flush()
+        for p in ps:
+            p.ctx.sync()  # sticky device status: candidate / keypoint capacity
+            p.ctx.stage_stats(reset=True)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            step()
-        if runner is not None:
-            runner.flush()   # the last step's gather is part of the timed work
+            for p in ps:
+                p.step()
+        for p in ps:
+            p.flush()   # the last step's gather is part of the timed work
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        ctx.sync()  # raises if any timed step overflowed a capacity
-        stats = ctx.stage_stats(reset=True)
-        kp_step = torch.tensor([float(bufs[0][2][-1].item())], dtype=torch.float64, device="cuda")
+        stats = {}
+        for p in ps:
+            p.ctx.sync()  # raises if any timed step overflowed a capacity
+            stats = p.ctx.stage_stats(reset=True)
+        kp_step = torch.tensor([float(sum(int(p.bufs[0][2][-1].item()) for p in ps))], dtype=torch.float64,
+                               device="cuda")
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -440,12 +484,26 @@ def main():
         return float(t.item()), stats, float(kp_step.item())
 
     want = (lambda leg_name: a.only in (None, leg_name))
-    exact = leg(siftgpu.SIFT_FLAG_PROFILE) if want("exact") else None
+    exact = prof = None
     verified, failed = ([], [])
-    if exact is not None and rank == 0:
-        verified, failed = verify_outputs(*bufs[0], R, C, B, a.octaves, seed_base)
-    fast = None if (a.no_fast or not want("fast")) else leg(siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
-    match = None if (a.no_match or rank != 0 or B < 2 or exact is None) else match_leg(ctx, a, bufs[0][1], bufs[0][2])
+    if want("exact"):
+        exact = leg(parts, 0)
+        if rank == 0:
+            verified, failed = verify_outputs([(p.b0, p.nb) + p.bufs[0] for p in parts], R, C, a.octaves,
+                                              seed_base)
+        prof = leg([serial], siftgpu.SIFT_FLAG_PROFILE)
+    fast = fast_prof = None
+    if not a.no_fast and want("fast"):
+        # one stream: with the HBM-heavy separable pyramid the 4-stream split
+        # measured slower (16.05 vs 15.4 ms per step on MI355X)
+        fast = leg([serial], siftgpu.SIFT_FLAG_FAST)
+        fast_prof = leg([serial], siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
+    match = None
+    if not (a.no_match or rank != 0 or B < 2 or exact is None):
+        serial.ctx.set_flags(0)
+        serial.compute(*serial.bufs[0])
+        serial.ctx.sync()
+        match = match_leg(serial.ctx, a, serial.bufs[0][1], serial.bufs[0][2])
     single = None
     if rank == 0 and world == 1 and not a.no_single and want("single"):
         single = single_image_leg(R, C, a.steps, a.warmup)
@@ -454,7 +512,8 @@ def main():
         tr = load_traffic()
         out = {"metric": METRIC}
         if exact is not None:
-            dt, stats, kp_total_step = exact
+            dt, _, kp_total_step = exact
+            pdt, stats, _ = prof   # stage times / rooflines: the serial profiled leg
             mpix = world * B * R * C * a.steps / 1e6
             value = mpix / dt
             # roofline of the dominant kernel: the exact octave blur (blur_octave_kernel)
@@ -494,7 +553,7 @@ def main():
                                        f"(N=8 x 64 = configs[3]), {a.octaves} octaves x 5 scales, exact mode",
                            "global_batch": world * B, "rows": R, "cols": C, "octaves": a.octaves,
                            "mode": "exact (bit-identical to the CPU path)",
-                           "parallelism": f"image-sharded x{world}" +
+                           "parallelism": f"image-sharded x{world}, {S} HIP streams x {B // S} images per GPU" +
                                           (", RCCL keypoint gather one step behind" if gathering else "")},
                 "output_verified": bool(verified) and not failed,
                 "output_verified_seeds": verified,
@@ -505,6 +564,12 @@ def main():
                             "algorithmic_GBs": round(pyr_bytes / (pyr_ms * 1e-3) / 1e9, 1) if pyr_ms else None,
                             "note": "B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes), SURVEY.md 8(d)"},
                 "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in stats.items()},
+                "serial_leg": {"ms_per_step": round(pdt / a.steps * 1e3, 3),
+                               "Mpix_per_s": round(mpix / pdt, 2),
+                               "note": "one context, the whole batch on one stream, HIP events around every "
+                                       "stage (SIFT_FLAG_PROFILE, no graph): the source of stages_ms_per_step, "
+                                       "roofline and descriptor; value is the streams leg (graph replay, no "
+                                       "events)"},
             })
             if failed:
                 out["output_failed_seeds"] = failed
@@ -518,7 +583,8 @@ def main():
                                                                      (d["ms"] * 1e-3), 1),
                                      "roofline": descriptor_roofline(tr, d)}
         if fast is not None:
-            fdt, fst, fkp = fast
+            fdt, _, fkp = fast
+            fst = fast_prof[1]
             mpix = world * B * R * C * a.steps / 1e6
             pf = fst.get("pyramid_fast", {"ms": 0.0, "bytes": 0.0, "launches": 0})
             gbs = pf["bytes"] / (pf["ms"] * 1e-3) / 1e9 if pf["ms"] else 0.0
@@ -527,7 +593,8 @@ def main():
                 "value": round(mpix / fdt, 2), "unit": "Mpix/s", "ms_per_step": round(fdt / a.steps * 1e3, 3),
                 "keypoints_per_s": round(fkp * a.steps / fdt, 1), "keypoints_per_step": int(fkp),
                 "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in fst.items()},
-                "note": "SIFT_FLAG_FAST: separable row/column Gaussian pyramid (pyramid_fast.hip) in front of "
+                "note": "one context, one stream, graph replay; SIFT_FLAG_FAST: separable row/column Gaussian "
+                        "pyramid (pyramid_fast.hip) in front of "
                         "the same exact DoG/extrema/orientation/descriptor kernels; not bit-exact (float "
                         "rounding of the pyramid), keypoint/descriptor match rates vs the CPU path are in "
                         "tests/test_gpu_fast.py"}
@@ -568,11 +635,12 @@ def main():
             if single is not None:
                 single["speedup_vs_cpu_1thread_keypoints_per_s"] = round(
                     single["keypoints_per_s"] / cb["keypoints_per_s"], 1)
-        if a.profile_json and exact is not None:
+        if a.profile_json and prof is not None:
             with open(a.profile_json, "w") as f:
-                json.dump(exact[1], f, indent=1)
+                json.dump(prof[1], f, indent=1)
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for p in parts + [serial]:
+        p.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -121,6 +121,52 @@ def _pipeline_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _parts_fake(part, rank, step, nb):
+    n = 3 + part + 2 * rank + step
+    offs = torch.tensor([n * i // nb for i in range(nb + 1)], dtype=torch.int32)
+    kp = torch.arange(n * 7, dtype=torch.int32).reshape(n, 7) + 10000 * part + 1000 * rank + 100 * step
+    return offs, kp
+
+
+def _parts_worker(rank, world, port, q):
+    """bench.py's streams layout at N > 1: several sub-batches per rank, each
+    with its own GatherPipeline, stepped in the same order on every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cap, sizes = 64, [2, 3]
+        got = {}
+        runners = []
+        for part, nb in enumerate(sizes):
+            pipe = sdist.GatherPipeline([nb] * world, cap, dst=0)
+            bufs = [(torch.zeros((cap, 7), dtype=torch.int32), torch.zeros((cap, 128)),
+                     torch.zeros(nb + 1, dtype=torch.int32)) for _ in range(2)]
+
+            def on_result(step, out, part=part):
+                ks, offs, _ = out
+                got[(part, step)] = ([k.clone() for k in ks], [o.clone() for o in offs])
+            runners.append(sdist.PipelinedSteps(pipe, bufs, with_desc=False, on_result=on_result))
+        for step in range(4):
+            for part, nb in enumerate(sizes):
+                def compute(k, d, o, part=part, nb=nb, step=step):
+                    offs, kp = _parts_fake(part, rank, step, nb)
+                    o[:] = offs
+                    k[:len(kp)] = kp
+                runners[part].step(compute)
+        for r in runners:
+            r.flush()
+        if rank == 0:
+            ok = sorted(got) == [(p, s) for p in range(len(sizes)) for s in range(4)]
+            for (part, step), (ks, os_) in got.items():
+                for r in range(world):
+                    offs, kp = _parts_fake(part, r, step, sizes[part])
+                    ok = ok and torch.equal(ks[r], kp) and torch.equal(os_[r], offs)
+            q.put(ok)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
 def _spawn(target, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -168,3 +214,16 @@ def test_gather_keypoints_world2():
         assert np.all(ds[r] == r + 1)
     assert shapes == [4, 0]
     assert uneven == ([4, 5], [[0, 1, 4], [0, 1, 2, 5]])
+
+
+def test_pipelined_parts_world2():
+    """Two sub-batches per rank, each gathered one step behind by its own
+    pipeline (bench.py --streams at N > 1): every part's every step arrives."""
+    procs, q = _spawn(_parts_worker)
+    try:
+        ok = q.get(timeout=120)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert [p.exitcode for p in procs] == [0, 0]
+    assert ok
