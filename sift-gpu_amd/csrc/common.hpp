@@ -105,6 +105,23 @@ __device__ __forceinline__ float exp32f(float v, const float* __restrict__ tab,
   return sc * tab[vi & 63] * poly;
 }
 
+// The same with the table held one entry per lane (lane j: tab[j]) and read
+// with a cross-lane permute instead of an LDS gather; every lane of the wave
+// must execute it.
+__device__ __forceinline__ float exp32f_v(float v, float tab_lane, const ExpConsts& k) {
+  v = v < k.lo ? k.lo : v;
+  v = k.hi < v ? k.hi : v;
+  v = v * k.prescale;
+  int vi = cv_round(v);
+  v = (v - (float)vi) * k.post;
+  int t = (vi >> 6) + 127;
+  t = !(t & ~255) ? t : t < 0 ? 0 : 255;
+  float sc = __int_as_float(t << 23);
+  float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
+  const float tv = __int_as_float(__builtin_amdgcn_ds_bpermute((vi & 63) << 2, __float_as_int(tab_lane)));
+  return sc * tv * poly;
+}
+
 // hal::fastAtan2 in degrees.
 struct AtanConsts {
   float p1, p3, p5, p7, eps;

@@ -79,7 +79,6 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   __shared__ __attribute__((aligned(16))) float rec[8 * kRecStride2];
   __shared__ int rows_tab[kGrp][kMaxWinRows];       // per row: (jlo + 64) | len << 16
   __shared__ float bc[kGrp][4];
-  __shared__ float etab[64];
   __shared__ int sord[kGrp];                        // this sub-batch's keypoint indices
   const int lane = threadIdx.x & 63;
   const int g = lane >> 3, q = lane & 7;
@@ -87,7 +86,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
   int n = A.img_kp_off[A.batch];
   if (n > A.kp_cap) n = A.kp_cap;
   const ExpConsts ek = A.mc->e;
-  etab[lane] = A.mc->exptab[lane];
+  const float etab_lane = A.mc->exptab[lane];  // lane j holds 2^(j/64) * A0 (exp32f_v)
 
   // XCD-aware split (speed only): blocks b and b+8 share an XCD, so XCD x takes
   // one contiguous eighth of the raster-ordered keypoints and its L2 sees the
@@ -237,7 +236,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       const float2 mo_raw = gimg[(long long)rcl * pitch + ccl];  // (Mag, Ori) of the pixel
       // invalid: (0, 0) -- border gradients are never written and may hold NaN
       const float2 mo = ok ? mo_raw : make_float2(0.f, 0.f);
-      const float w = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab, ek);
+      const float w = exp32f_v((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
       float obin = (mo.y - ori) * bins_per_rad;
       const float mag = mo.x * w;
       int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
