@@ -21,8 +21,9 @@ Outside the timed region rank 0 checks its image 0 (seed 0) -- and seeds 31
 and 63 at the default shape -- against the CPU path's SHA-256 digests
 (tests/golden) and reports "output_verified".  Further legs (rank 0, N=1
 unless noted): SIFT_FLAG_FAST (separable pyramid, HBM roofline), configs[1]
-single-image latency (hipGraph replay, 4 octaves), the knnMatch leg, and the
-CPU baseline (oracle, 1 thread + image-parallel on the host's cores).
+single-image latency (hipGraph replay, 4 octaves), configs[4] (one 8K image,
+output checked, pyramid rooflines at C5), the knnMatch leg, and the CPU
+baseline (oracle, 1 thread + image-parallel on the host's cores).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).  Rank 0 prints one JSON line.
@@ -72,7 +73,8 @@ def parse():
     p.add_argument("--no-single", action="store_true", help="skip the configs[1] single-image leg")
     p.add_argument("--streams", type=int, default=4,
                    help="timed legs: the per-GPU batch as this many sub-batches, one context + HIP stream each")
-    p.add_argument("--only", default=None, choices=[None, "exact", "fast", "single"],
+    p.add_argument("--no-8k", action="store_true", help="skip the configs[4] 7680x4320 leg")
+    p.add_argument("--only", default=None, choices=[None, "exact", "fast", "single", "8k"],
                    help="profiling runs: time only this leg")
     p.add_argument("--profile-json", default=None, help="also write per-stage stats here")
     return p.parse_args()
@@ -318,6 +320,72 @@ def single_image_leg(R, C, steps, warmup, octaves=4):
     return out
 
 
+# ---- 8K single image (configs[4]) ---------------------------------------------
+def eightk_leg(steps, warmup, R8=4320, C8=7680):
+    """configs[4]: one 7680x4320 synthetic image (seed 0), 5 octaves, exact
+    mode, resident in HBM: graph replay + sift_sync latency, output checked
+    against the CPU path's digests (tests/golden/synth0_4320x7680.npz).  Then
+    the pyramid rooflines SURVEY 8(d) d3 asks for at C5: the exact octave blur
+    and the SIFT_FLAG_FAST separable pyramid, from PROFILE-mode HIP events."""
+    out = {}
+    g = np.load(os.path.join(GOLDEN, "synth0_4320x7680.npz"), allow_pickle=False)
+    with siftgpu.Context(R8, C8, 1, device=torch.cuda.current_device()) as ctx:
+        img = torch.empty((1, R8, C8), dtype=torch.float32, device="cuda")
+        ctx.synth_images(img.data_ptr(), 1, R8, C8, C8, R8 * C8, seed_base=0)
+        cap = 400000
+        kpts = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
+        desc = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
+        offs = torch.empty((2,), dtype=torch.int32, device="cuda")
+
+        def call():
+            ctx.detect_compute_batch(img.data_ptr(), 1, R8, C8, C8, R8 * C8, kpts.data_ptr(), desc.data_ptr(), cap,
+                                     offs.data_ptr())
+            ctx.sync()
+        for _ in range(warmup + 1):
+            call()
+        ts = []
+        for _ in range(max(steps, 5)):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        lat = float(np.median(ts))
+        n = int(offs[1].item())
+        verified = n == int(g["n"]) and _sha(kpts[:n].cpu().numpy()) == str(g["kp_sha"]) and \
+            _sha(desc[:n].cpu().numpy()) == str(g["desc_sha"])
+        px = sum((R8 >> o) * (C8 >> o) for o in range(5))
+        roof = {}
+        for name, flags, stage in (("exact_blur_octave", siftgpu.SIFT_FLAG_PROFILE, "blur_octave"),
+                                   ("fast_pyramid", siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST,
+                                    "pyramid_fast")):
+            ctx.set_flags(flags)
+            call()
+            ctx.stage_stats(reset=True)
+            reps = max(steps, 5)
+            for _ in range(reps):
+                call()
+            st = ctx.stage_stats(reset=True).get(stage)
+            if not st or not st["ms"]:
+                continue
+            if stage == "blur_octave":
+                tf = st["flops"] / (st["ms"] * 1e-3) / 1e12
+                roof[name] = {"bound": "valu", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS,
+                              "unit": "TFLOP/s", "frac": round(tf / FP32_PEAK_TFLOPS, 4),
+                              "ms_per_image": round(st["ms"] / reps, 4)}
+            else:
+                gbs = st["bytes"] / (st["ms"] * 1e-3) / 1e9
+                roof[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(gbs / HBM_PEAK_GBS, 4), "ms_per_image": round(st["ms"] / reps, 4),
+                              "algorithmic_bytes": round(24.0 * px)}
+        ctx.set_flags(0)
+    out.update({"config": f"configs[4]: one {C8}x{R8} synthetic image (seed 0), 5 octaves x 5 scales, exact mode",
+                "latency_ms": round(lat * 1e3, 3), "Mpix_per_s": round(R8 * C8 / 1e6 / lat, 1),
+                "keypoints": n, "keypoints_per_s": round(n / lat, 1), "output_verified": bool(verified),
+                "roofline": roof,
+                "note": "latency = median wall time of sift_detect_compute_batch(batch 1) + sift_sync, image "
+                        "resident in HBM (graph replay); roofline legs use PROFILE-mode HIP events per stage"})
+    return out
+
+
 # ---- knnMatch leg (SURVEY 8(f) f2) ---------------------------------------------
 def match_leg(ctx, a, desc, offs):
     """src/main.cpp:27 on the batch's own output: knnMatch(k=2) of image 1's
@@ -507,6 +575,9 @@ def main():
     single = None
     if rank == 0 and world == 1 and not a.no_single and want("single"):
         single = single_image_leg(R, C, a.steps, a.warmup)
+    eightk = None
+    if rank == 0 and world == 1 and not a.no_8k and want("8k"):
+        eightk = eightk_leg(a.steps, a.warmup)
 
     if rank == 0:
         tr = load_traffic()
@@ -626,6 +697,8 @@ def main():
                 out["match"]["cpu_baseline"] = match_cpu_baseline(match)
         if single is not None:
             out["single_image"] = single
+        if eightk is not None:
+            out["image_8k"] = eightk
         if cpu is not None:
             out.update(cpu)
             cb = cpu["cpu_baseline"]

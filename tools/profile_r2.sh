@@ -23,11 +23,11 @@ run() {  # name, timeout, rocprof args..., -- cmd
 }
 timeout -k 5 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 run trace 400 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --no-single --no-match $ARGS
+  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match $ARGS
 run fetch 300 --kernel-trace --pmc FETCH_SIZE -T -d $OUT/fetch -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --no-single --no-match --steps 1 --warmup 1 $ARGS
+  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match --steps 1 --warmup 1 $ARGS
 run write 300 --kernel-trace --pmc WRITE_SIZE -T -d $OUT/write -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --no-single --no-match --steps 1 --warmup 1 $ARGS
+  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match --steps 1 --warmup 1 $ARGS
 run cal_f 120 --kernel-trace --pmc FETCH_SIZE -d $OUT/cal_f -o run --output-format csv -- ./tools/fetch_calib
 run cal_w 120 --kernel-trace --pmc WRITE_SIZE -d $OUT/cal_w -o run --output-format csv -- ./tools/fetch_calib
 i=0
