@@ -1,7 +1,9 @@
 #!/bin/bash
 # rocprofv3 evidence for one tree (run on the GPU box; every pass is its own
 # process, counters never combined with runtime/sys tracing):
-#   trace      --kernel-trace --stats over bench.py (exact + fast legs)
+#   trace      --kernel-trace --stats over bench.py (exact + fast legs; --streams 1:
+#              every launch covers the whole 64-image batch, none overlaps another,
+#              so per-launch durations and bytes match bench.py's serial leg)
 #   fetch/write  --pmc FETCH_SIZE / WRITE_SIZE over bench.py (one step each)
 #   cal_f/cal_w  the same counters over tools/fetch_calib (known byte counts)
 #   sqA..sqC   SQ / GRBM / TCC counter groups over tools/stage_bench.py for the
@@ -23,11 +25,11 @@ run() {  # name, timeout, rocprof args..., -- cmd
 }
 timeout -k 5 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 run trace 400 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match $ARGS
+  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match --streams 1 $ARGS
 run fetch 300 --kernel-trace --pmc FETCH_SIZE -T -d $OUT/fetch -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match --steps 1 --warmup 1 $ARGS
+  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match --streams 1 --steps 1 --warmup 1 $ARGS
 run write 300 --kernel-trace --pmc WRITE_SIZE -T -d $OUT/write -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match --steps 1 --warmup 1 $ARGS
+  python3 bench.py --no-cpu-baseline --no-single --no-8k --no-match --streams 1 --steps 1 --warmup 1 $ARGS
 run cal_f 120 --kernel-trace --pmc FETCH_SIZE -d $OUT/cal_f -o run --output-format csv -- ./tools/fetch_calib
 run cal_w 120 --kernel-trace --pmc WRITE_SIZE -d $OUT/cal_w -o run --output-format csv -- ./tools/fetch_calib
 i=0
