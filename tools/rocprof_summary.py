@@ -114,6 +114,20 @@ def main():
     for grp in ("sq1", "sq2", "sq3", "sqF1", "sqF2", "sqF3"):
         for k, v in counters(os.path.join(src, grp, "run_counter_collection.csv")).items():
             sq[k].update(v)
+    # shader clock per kernel: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 /
+    # the dispatch's duration in the same counter pass
+    clock = {}
+    for grp in ("sq3", "sqF3"):
+        path = os.path.join(src, grp, "run_kernel_trace.csv")
+        if not os.path.exists(path):
+            continue
+        durs = defaultdict(list)
+        for r in csv.DictReader(open(path)):
+            durs[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        for k, ds in durs.items():
+            g = sq.get(k, {}).get("GRBM_GUI_ACTIVE")
+            if g and ds:
+                clock[k] = g / 8 / (sum(ds) / len(ds))
     if sq:
         lines += ["", "## SQ counters (tools/stage_bench.py, one step of the 64 x 1080p batch)", "",
                   "Per dispatch, averaged over the dispatches of a kernel.  SQ_WAVE_CYCLES / SQ_WAIT_* / "
@@ -121,7 +135,8 @@ def main():
                   "wave time; VALU issue util = SQ_ACTIVE_INST_VALU x 4 / (SQ_BUSY_CYCLES x 4 SIMDs ... see "
                   "json); clock = GRBM_GUI_ACTIVE / 8 XCDs / duration.", "",
                   "| kernel | waves | VALU instr/wave | LDS instr/wave | wait (s_waitcnt/barrier) | issue stall | "
-                  "active | LDS bank-conflict cycles / LDS active | L2 hit |", "|---|---|---|---|---|---|---|---|---|"]
+                  "active | LDS bank-conflict cycles / LDS active | L2 hit | clock GHz |",
+                  "|---|---|---|---|---|---|---|---|---|---|"]
         for k, v in sorted(sq.items()):
             if "SQ_WAVES" not in v:
                 continue
@@ -134,11 +149,18 @@ def main():
                 f"{v.get('SQ_INSTS_LDS', 0) / v['SQ_WAVES']:.0f} | {v.get('SQ_WAIT_ANY', 0) / wc:.2f} | "
                 f"{v.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | {v.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f} | "
                 f"{v.get('SQ_LDS_BANK_CONFLICT', 0) / lds_act:.2f} | "
-                f"{hit / (hit + miss) if hit + miss else 0:.2f} |")
+                f"{hit / (hit + miss) if hit + miss else 0:.2f} | "
+                f"{clock[k]:.2f} |" if k in clock else
+                f"| {k} | {v['SQ_WAVES']:.0f} | {v.get('SQ_INSTS_VALU', 0) / v['SQ_WAVES']:.0f} | "
+                f"{v.get('SQ_INSTS_LDS', 0) / v['SQ_WAVES']:.0f} | {v.get('SQ_WAIT_ANY', 0) / wc:.2f} | "
+                f"{v.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | {v.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f} | "
+                f"{v.get('SQ_LDS_BANK_CONFLICT', 0) / lds_act:.2f} | "
+                f"{hit / (hit + miss) if hit + miss else 0:.2f} | - |")
     with open(os.path.join(out, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
-        json.dump({"bench": bench, "calibration": cal, "kernels": summary, "sq": sq}, f, indent=1)
+        json.dump({"bench": bench, "calibration": cal, "kernels": summary, "sq": sq, "clock_GHz": clock}, f,
+                  indent=1)
     # VALU / LDS wave-instructions per dispatch (SQ pass over tools/stage_bench.py,
     # the same 64 x 1080p batch): bench.py's VALU-issue rooflines
     for name, v in sq.items():
