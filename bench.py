@@ -363,7 +363,10 @@ def eightk_leg(steps, warmup, R8=4320, C8=7680):
             reps = max(steps, 5)
             for _ in range(reps):
                 call()
-            st = ctx.stage_stats(reset=True).get(stage)
+            sts = ctx.stage_stats(reset=True)
+            st = sts.get(stage)
+            if stage == "blur_octave" and "blur_octave_sym" in sts:  # both blur forms: one figure
+                st = {k: (st or {}).get(k, 0) + sts["blur_octave_sym"][k] for k in ("ms", "flops")}
             if not st or not st["ms"]:
                 continue
             if stage == "blur_octave":
@@ -587,26 +590,40 @@ def main():
             pdt, stats, _ = prof   # stage times / rooflines: the serial profiled leg
             mpix = world * B * R * C * a.steps / 1e6
             value = mpix / dt
-            # roofline of the dominant kernel: the exact octave blur (blur_octave_kernel)
-            bo = stats.get("blur_octave", {"ms": 0, "flops": 0, "bytes": 0, "launches": 0})
-            per_launch_ms = bo["ms"] / max(bo["launches"], 1)
-            tflops = (bo["flops"] / max(bo["launches"], 1)) / (per_launch_ms * 1e-3) / 1e12 if per_launch_ms else 0.0
-            traffic, tsrc = traffic_of(tr, "blur_octave_kernel")
-            roof = {"bound": "valu", "achieved": round(tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                    "traffic_algorithmic": round(bo["bytes"] / max(bo["launches"], 1)),
-                    "traffic_source": tsrc,
-                    "kernel": "blur_octave_kernel",
-                    "avg_launch_ms": round(per_launch_ms, 4),
-                    "valu_issue_frac": valu_issue_frac(tr, "blur_octave_kernel", per_launch_ms),
-                    "note": "exact-mode 2-D blur is fp32-VALU bound, no MFMA; peak = the fp32 vector peak "
-                            "(FMA counted as 2 flops); the parity contract forbids FMA, so each tap is one "
-                            "multiply + one add instruction and the ceiling is frac 0.5; flops = 2 x taps per "
-                            "launch (one octave, 4 scales, whole batch); traffic = HBM bytes per launch from "
-                            "the committed rocprofv3 PMC pass (calibrated FETCH_SIZE/WRITE_SIZE); "
-                            "valu_issue_frac = SQ_INSTS_VALU per launch (same PMC pass) / launch time / the "
-                            "wave64 VALU issue peak (256 CU x 4 SIMD x 2.4 GHz / 2 cycles)"}
-            pyr_ms = sum(stats[k]["ms"] for k in ("blur_base", "blur_octave", "decimate", "dog") if k in stats)
+            # roofline of the dominant kernel: the exact octave blur -- octave 0
+            # in scatter form (blur_sym_kernel) when the library chose it for
+            # this launch size, the 2-D tiles (blur_octave_kernel) otherwise
+            def blur_roof(stage, kernel):
+                bo = stats.get(stage)
+                if not bo or not bo["launches"]:
+                    return None
+                per_launch_ms = bo["ms"] / bo["launches"]
+                tflops = (bo["flops"] / bo["launches"]) / (per_launch_ms * 1e-3) / 1e12 if per_launch_ms else 0.0
+                traffic, tsrc = traffic_of(tr, kernel)
+                r = {"bound": "valu", "achieved": round(tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_algorithmic": round(bo["bytes"] / bo["launches"]),
+                     "traffic_source": tsrc, "kernel": kernel, "launches_per_step": bo["launches"] // a.steps,
+                     "avg_launch_ms": round(per_launch_ms, 4),
+                     "valu_issue_frac": valu_issue_frac(tr, kernel, per_launch_ms),
+                     "note": "exact-mode 2-D blur is fp32-VALU bound, no MFMA; peak = the fp32 vector peak "
+                             "(FMA counted as 2 flops); flops = 2 x taps per launch, algorithmic (the "
+                             "reference's chain: one multiply + one add per tap, FMA forbidden by the parity "
+                             "contract), 4 scales x the whole batch; traffic = HBM bytes per launch from the "
+                             "committed rocprofv3 PMC pass (calibrated FETCH_SIZE/WRITE_SIZE); valu_issue_frac = "
+                             "SQ_INSTS_VALU per launch (same PMC pass) / launch time / the wave64 VALU issue peak "
+                             "(256 CU x 4 SIMD x 2.4 GHz / 2 cycles)"}
+                if kernel == "blur_sym_kernel":
+                    r["note"] += ("; scatter form: K[a][b] = K[-a][b], so each multiply serves kernel rows +a "
+                                  "and -a of two outputs -- (2w+1)(w+1) multiplies + (2w+1)^2 adds per output "
+                                  "instead of 2(2w+1)^2, same chain, bit-exact -- which is why frac can pass 0.5")
+                return r
+            sym_used = "blur_octave_sym" in stats
+            roof = blur_roof("blur_octave_sym", "blur_sym_kernel") if sym_used else \
+                blur_roof("blur_octave", "blur_octave_kernel")
+            roof_gather = blur_roof("blur_octave", "blur_octave_kernel") if sym_used else None
+            pyr_ms = sum(stats[k]["ms"] for k in ("blur_base", "blur_octave", "blur_octave_sym", "decimate", "dog")
+                         if k in stats)
             pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
             out.update({
                 "value": round(value, 2),
@@ -631,6 +648,7 @@ def main():
                 "keypoints_per_s": round(kp_total_step * a.steps / dt, 1),
                 "keypoints_per_step": int(kp_total_step),
                 "roofline": roof,
+                "roofline_octaves_2d_tiles": roof_gather,
                 "pyramid": {"ms_per_step": round(pyr_ms / a.steps, 3),
                             "algorithmic_GBs": round(pyr_bytes / (pyr_ms * 1e-3) / 1e9, 1) if pyr_ms else None,
                             "note": "B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes), SURVEY.md 8(d)"},

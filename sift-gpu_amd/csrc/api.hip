@@ -103,9 +103,9 @@ struct StageRec {
 
 const char* const kStageNames[] = {"blur_base", "blur_octave", "decimate", "dog", "extrema",
                                    "refine_orient", "emit", "descriptor", "upload", "download",
-                                   "blur_1d", "pyramid_fast", "match"};
+                                   "blur_1d", "pyramid_fast", "match", "blur_octave_sym"};
 enum Stage { ST_BLUR_BASE, ST_BLUR_OCT, ST_DECIMATE, ST_DOG, ST_EXTREMA, ST_REFINE, ST_EMIT,
-             ST_DESC, ST_UPLOAD, ST_DOWNLOAD, ST_BLUR1D, ST_PYR_FAST, ST_MATCH, ST_N };
+             ST_DESC, ST_UPLOAD, ST_DOWNLOAD, ST_BLUR1D, ST_PYR_FAST, ST_MATCH, ST_BLUR_SYM, ST_N };
 
 template <typename T>
 hipError_t dmalloc(T** p, size_t count) {
@@ -136,6 +136,9 @@ struct sift_ctx {
   size_t coef_gen_cap = 0;
   int wsz[4] = {0, 0, 0, 0};
   int w_base = 0;
+  bool sym_blur = false;          // symmetric scatter blur (blur.hip) for the base and octave scales
+  int sym_min = 256;              // ... for launches of >= sym_min 64-column strips x images
+  int sym_rows = 1000;            //     of >= sym_rows rows (a tall plane: little halo per chunk)
   size_t coef_base_off = 0, coef_oct_off = 0;
   MathConsts* d_mc = nullptr;
   DetectBufs D{};
@@ -298,6 +301,10 @@ int alloc_candidates(sift_ctx* c, int cap) {
 
 double plane_px(const Layout& L, int o) { return (double)L.oct[o].rows * L.oct[o].cols; }
 
+bool use_sym_blur(const sift_ctx* c, int rows, int cols, int batch) {
+  return c->sym_blur && rows >= c->sym_rows && (long long)((cols + 63) / 64) * batch >= c->sym_min;
+}
+
 // Gaussian pyramid (src/sift.cpp:229-263) + DoG (:265-283) for a batch whose
 // input planes are described by src.  Async on c->stream.
 void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool with_dog) {
@@ -322,8 +329,11 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
     const double px = plane_px(L, 0) * batch;
     const int k = 2 * c->w_base + 1;
     StageScope s(c, ST_BLUR_BASE, 2.0 * k * k * px, 8.0 * px);
-    launch_blur_plane(st, c->w_base, c->d_coef + c->coef_base_off, src, c->d_gpyr + L.oct[0].g_off[0],
-                      L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
+    if (use_sym_blur(c, L.oct[0].rows, L.oct[0].cols, batch))
+      launch_blur_base_sym(st, src, c->d_gpyr + L.oct[0].g_off[0], L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
+    else
+      launch_blur_plane(st, c->w_base, c->d_coef + c->coef_base_off, src, c->d_gpyr + L.oct[0].g_off[0],
+                        L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
   }
   for (int o = 0; o < L.n_oct; ++o) {
     const double px = plane_px(L, o) * batch;
@@ -334,8 +344,12 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
     {
       double taps = 0;
       for (int q = 0; q < 4; ++q) taps += (double)(2 * c->wsz[q] + 1) * (2 * c->wsz[q] + 1);
-      StageScope s(c, ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
-      launch_blur_octave(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch);
+      const bool sym = use_sym_blur(c, L.oct[o].rows, L.oct[o].cols, batch);
+      StageScope s(c, sym ? ST_BLUR_SYM : ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
+      if (sym)
+        launch_blur_octave_sym(st, L, o, c->d_gpyr, batch);
+      else
+        launch_blur_octave(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch);
     }
     if (with_dog) {
       StageScope s(c, ST_DOG, 4.0 * px, 36.0 * px);
@@ -571,7 +585,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   // and sig[1..4] (src/sift.cpp:240-245), each through getGaussianKernel(float).
   std::vector<float> coefs;
   float sig_f[4] = {0, 0, 0, 0};
-  const float sb = (float)sqrt(kSigma * kSigma + 0.2 * 0.2);
+  float sb = 0;
+  sift_sigmas(&sb, sig_f);
   {
     const int ks = gaussian_kernel_host(sb, nullptr);
     c->w_base = ks / 2;
@@ -579,11 +594,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     coefs.resize(ks * ks);
     gaussian_kernel_host(sb, coefs.data());
     c->coef_oct_off = coefs.size();
-    const double k = pow(2.0, 1.0 / kLayers);
     for (int i = 1; i < kScales; ++i) {
-      const double tot = pow(k * 1.0, (double)i) * kSigma;
-      const float sg = (float)sqrt(tot * tot - kSigma * kSigma);
-      sig_f[i - 1] = sg;
+      const float sg = sig_f[i - 1];
       const int kk = gaussian_kernel_host(sg, nullptr);
       c->wsz[i - 1] = kk / 2;
       const size_t at = coefs.size();
@@ -593,6 +605,20 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   }
   if (c->w_base != 4 || c->wsz[0] != 4 || c->wsz[1] != 8 || c->wsz[2] != 12 || c->wsz[3] != 18)
     return bail(SIFT_E_INVALID);  // the octave kernel is unrolled for these widths
+  {
+    // the scatter-form blur carries these tables as literals; the gather-form
+    // kernels (same chain, twice the multiplies) stay as the path for any
+    // mismatch and for A/B runs (SIFT_HIP_BLUR_GATHER=1)
+    const char* e = getenv("SIFT_HIP_BLUR_GATHER");
+    c->sym_blur = sym_tables_match(coefs.data()) && !(e && atoi(e) != 0);
+    // a scatter walk is a tall column strip (its halo is recomputed per
+    // chunk), so it needs many strips to fill the chip; small launches (one
+    // 1080p image) keep the 2-D tiles.  SIFT_HIP_SYM_MIN=0 forces it (tests).
+    const char* m = getenv("SIFT_HIP_SYM_MIN");
+    if (m) c->sym_min = atoi(m);
+    const char* r = getenv("SIFT_HIP_SYM_ROWS_MIN");
+    if (r) c->sym_rows = atoi(r);
+  }
   c->fast_taps.resize(fast_coefs_size());
   if (fast_coefs_host(sb, sig_f, c->fast_taps.data()) != 0) return bail(SIFT_E_INVALID);
   MathConsts mc;

@@ -25,24 +25,11 @@
 #include "common.hpp"
 
 #include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 namespace sift {
-
-// ---- coefficients (host), src/sift.cpp:95-108 -----------------------------
-int gaussian_kernel_host(float sigma, float* coeff) {
-  int w = (int)floor(3 * sigma);
-  int size = 2 * w + 1;
-  double norm = 1. / (2 * kRefPi * sigma * sigma);  // double chain
-  double den = (double)(2 * sigma * sigma);          // float chain, then double
-  if (coeff)
-    for (int a = -w; a <= w; ++a)
-      for (int b = -w; b <= w; ++b) {
-        double g = norm * exp(-(a * a + b * b) * 1. / den);
-        g = g * 8192;
-        coeff[(a + w) * size + (b + w)] = (float)g;
-      }
-  return size;
-}
 
 // ---- exact 2-D tile -----------------------------------------------------------
 constexpr int kPX = 8;    // outputs per lane along a row
@@ -263,6 +250,306 @@ void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, con
   A.pad_ = 0;
   dim3 grid((O.cols + kTileW - 1) / kTileW, (O.rows + kTY - 1) / kTY, batch * 4);
   hipLaunchKernelGGL(blur_octave_kernel, grid, dim3(256), lds_bytes_for(18), st, A);
+}
+
+// ---- exact 2-D blur, symmetric scatter form (the SIFT_NCL tables) ----------
+// Same float chain per output as blur_tile, about 24 % fewer VALU instructions.
+// K[a][b] depends on a^2 + b^2 only (src/sift.cpp:103), so the product
+// src'(r, x+b) * K[a][b] that output row r - a needs (its kernel row +a) is the
+// same float as the one output row r + a needs (kernel row -a).  A lane owns
+// one output column and walks down the source rows; accumulators for the
+// 2w+1 outputs a source row touches stay in registers, and each source row is
+// applied to all of them at once: per column offset b (ascending) and
+// |a| = 0..w, one multiply feeds two adds.  Every output still receives its
+// terms row by row (ascending r, i.e. ascending kernel row) and within a row
+// by ascending b -- the reference's raster order -- so the result is the
+// reference's chain bit for bit.  Rows outside [0, rows-1) contribute +0.0
+// products (getSubMatrix padding, :116), which leave any sum that starts at
+// +0.0 unchanged, so they are skipped.  Multiplies: (2w+1)(w+1) instead of
+// (2w+1)^2 per output; adds unchanged.
+//
+// The tables are compile-time constants (build/sym_coefs.inc, printed by
+// gen_sym_coefs.cpp from the library's own gauss_host.hpp): every multiply
+// takes its coefficient as a literal operand, no scalar loads in the walk.
+// sym_tables_match() re-checks them against the context's tables.
+#include "../build/sym_coefs.inc"
+
+template <int T> struct SymTab;
+template <> struct SymTab<0> { static constexpr int W = kSymW0; };
+template <> struct SymTab<1> { static constexpr int W = kSymW1; };
+template <> struct SymTab<2> { static constexpr int W = kSymW2; };
+template <> struct SymTab<3> { static constexpr int W = kSymW3; };
+template <> struct SymTab<4> { static constexpr int W = kSymW4; };
+
+template <int T>
+__device__ __forceinline__ constexpr float symk(int a, int b) {
+  if constexpr (T == 0) return kSymK0[a][b];
+  else if constexpr (T == 1) return kSymK1[a][b];
+  else if constexpr (T == 2) return kSymK2[a][b];
+  else if constexpr (T == 3) return kSymK3[a][b];
+  else return kSymK4[a][b];
+}
+
+static_assert(kSymW0 == 4 && kSymW1 == 4 && kSymW2 == 8 && kSymW3 == 12 && kSymW4 == 18,
+              "SIFT_NCL kernel widths");
+
+// One empty asm naming every product register: the multiplies of a column
+// offset stay ahead of all its adds (separate asm statements would let the
+// scheduler sink each multiply next to its first add again).
+#define SIFT_V(i) "+v"(p[i])
+__device__ __forceinline__ void pin_regs(float (&p)[5]) {
+  asm volatile("" : SIFT_V(0), SIFT_V(1), SIFT_V(2), SIFT_V(3), SIFT_V(4));
+}
+__device__ __forceinline__ void pin_regs(float (&p)[9]) {
+  asm volatile("" : SIFT_V(0), SIFT_V(1), SIFT_V(2), SIFT_V(3), SIFT_V(4), SIFT_V(5), SIFT_V(6), SIFT_V(7),
+               SIFT_V(8));
+}
+__device__ __forceinline__ void pin_regs(float (&p)[13]) {
+  asm volatile("" : SIFT_V(0), SIFT_V(1), SIFT_V(2), SIFT_V(3), SIFT_V(4), SIFT_V(5), SIFT_V(6), SIFT_V(7),
+               SIFT_V(8), SIFT_V(9), SIFT_V(10), SIFT_V(11), SIFT_V(12));
+}
+__device__ __forceinline__ void pin_regs(float (&p)[19]) {
+  asm volatile("" : SIFT_V(0), SIFT_V(1), SIFT_V(2), SIFT_V(3), SIFT_V(4), SIFT_V(5), SIFT_V(6), SIFT_V(7),
+               SIFT_V(8), SIFT_V(9), SIFT_V(10), SIFT_V(11), SIFT_V(12), SIFT_V(13), SIFT_V(14), SIFT_V(15),
+               SIFT_V(16), SIFT_V(17), SIFT_V(18));
+}
+#undef SIFT_V
+
+// Source rows per loop step: narrow kernels take several so the loop and
+// staging overhead is spread over enough arithmetic.
+template <int W> struct SymRows { static constexpr int R = W <= 4 ? 4 : W <= 8 ? 2 : 1; };
+template <int W> struct SymSeg {
+  static constexpr int SEG = 64 + 2 * W;  // staged source columns [x0 - w, x0 + 64 + w)
+  static constexpr int RING = 2 * SymRows<W>::R * SEG;  // two halves of R staged rows
+};
+constexpr int kSymRing = SymSeg<4>::RING;  // the largest (R = 4)
+static_assert(SymSeg<8>::RING <= kSymRing && SymSeg<12>::RING <= kSymRing && SymSeg<18>::RING <= kSymRing,
+              "ring size");
+
+struct SymArgs {
+  const float* src;
+  long long s_pitch, s_img;
+  float* dst[4];       // per slot, image 0
+  long long d_pitch, d_img;
+  int rows, cols, strips, batch;
+  int start[5];        // first wave of each slot; start[nslot] = grid size
+  int chunk[4];        // output rows per wave, per slot
+};
+
+// One wave: output columns [x0, x0 + 64) x rows [y0, y1) of one plane.
+template <int T>
+__device__ __forceinline__ void sym_walk(const SymArgs& A, int slot, int local, float* __restrict__ ring) {
+  constexpr int W = SymTab<T>::W, R = SymRows<W>::R, NA = 2 * W + R, SEG = SymSeg<W>::SEG;
+  const int lane = threadIdx.x & 63;
+  const int strip = local % A.strips, t = local / A.strips;
+  const int b = t % A.batch, ck = t / A.batch;
+  const int x0 = strip * 64, y0 = ck * A.chunk[slot], y1 = min(y0 + A.chunk[slot], A.rows);
+  const int rows = A.rows, cols = A.cols;
+  const float* __restrict__ src = A.src + b * A.s_img;
+  float* __restrict__ dst = A.dst[slot] + b * A.d_img;
+  const int xo = x0 + lane;
+  // staging: lane stages segment elements lane and lane + 64 (< SEG)
+  const int cl = x0 - W + lane, ch = cl + 64;
+  const bool okl = cl >= 0 && cl < cols - 1;
+  const bool okh = lane < 2 * W && ch >= 0 && ch < cols - 1;
+  const float* pl = src + (okl ? cl : 0);
+  const float* ph = src + (okh ? ch : 0);
+  float vl[R], vh[R];
+  auto fetch = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long long ro = (long long)min(max(r0 + i, 0), rows - 1) * A.s_pitch;
+      vl[i] = pl[ro];
+      vh[i] = okh ? ph[ro] : 0.f;
+    }
+  };
+  auto stage = [&](int h) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      float* d = ring + (h * R + i) * SEG;
+      d[lane] = okl ? vl[i] : 0.f;
+      if (lane < 2 * W) d[lane + 64] = vh[i];
+    }
+  };
+  float acc[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) acc[k] = 0.f;
+  // acc[k] is output row r0 - W + k; rows above 0 add nothing, so the walk
+  // starts at the first row that can: max(y0 - W, 0)
+  int r0 = max(y0 - W, 0);
+  fetch(r0);
+  stage(0);
+  int h = 0;
+  for (; r0 < y1 + W; r0 += R) {
+    fetch(r0 + R);  // next step's rows, in flight during this step
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int r = r0 + i;
+      if (r < rows - 1) {  // uniform; r >= 0 always
+        const float* lr = ring + (h * R + i) * SEG + lane;
+        float x[2 * W + 1];
+#pragma unroll
+        for (int c = 0; c <= 2 * W; ++c) x[c] = lr[c];
+#pragma unroll
+        for (int c = 0; c <= 2 * W; ++c) {
+          const int bb = c < W ? W - c : c - W;
+          // the w+1 products of this column offset first, in distinct
+          // registers (pinned by the empty asm), then their 2w+1 adds: no add
+          // waits on the multiply right before it
+          float p[W + 1];
+#pragma unroll
+          for (int a = 0; a <= W; ++a) p[a] = x[c] * symk<T>(a, bb);
+          pin_regs(p);
+#pragma unroll
+          for (int a = 0; a <= W; ++a) {
+            acc[i + W - a] = acc[i + W - a] + p[a];  // output r - a (kernel row +a)
+            if (a) acc[i + W + a] = acc[i + W + a] + p[a];  // output r + a (kernel row -a)
+          }
+        }
+      }
+      const int y = r - W;  // complete: its last kernel row was r
+      if (y >= y0 && y < y1 && xo < cols) dst[(long long)y * A.d_pitch + xo] = acc[i] / 8192.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NA - R; ++k) acc[k] = acc[k + R];
+#pragma unroll
+    for (int k = NA - R; k < NA; ++k) acc[k] = 0.f;
+    h ^= 1;
+    stage(h);
+  }
+}
+
+// Waves are independent (one 64-lane workgroup each).  The octave kernel's
+// slots run in launch order, widest kernel first: slot s blurs scale 4 - s.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void blur_sym_kernel(SymArgs A) {
+  __shared__ float ring[kSymRing];
+  const int wid = blockIdx.x;
+  const int slot = wid >= A.start[3] ? 3 : wid >= A.start[2] ? 2 : wid >= A.start[1] ? 1 : 0;
+  const int local = wid - A.start[slot];
+  switch (slot) {
+    case 0: sym_walk<4>(A, 0, local, ring); break;
+    case 1: sym_walk<3>(A, 1, local, ring); break;
+    case 2: sym_walk<2>(A, 2, local, ring); break;
+    default: sym_walk<1>(A, 3, local, ring); break;
+  }
+}
+
+// The octave-0 base (createInitialImage's blur of the input, table 0).
+__global__ __launch_bounds__(64) void blur_sym_base_kernel(SymArgs A) {
+  __shared__ float ring[SymSeg<kSymW0>::RING];
+  sym_walk<0>(A, 0, blockIdx.x, ring);
+}
+
+bool sym_tables_match(const float* coefs) {
+  // api.hip's layout: the base table, then sig[1..4]'s, each (2w+1)^2 row-major
+  const int ws[5] = {kSymW0, kSymW1, kSymW2, kSymW3, kSymW4};
+  size_t at = 0;
+  for (int t = 0; t < 5; ++t) {
+    const int w = ws[t], ks = 2 * w + 1;
+    for (int a = -w; a <= w; ++a)
+      for (int b = -w; b <= w; ++b) {
+        const int aa = a < 0 ? -a : a, bb = b < 0 ? -b : b;
+        float k = 0;
+        switch (t) {
+          case 0: k = kSymK0[aa][bb]; break;
+          case 1: k = kSymK1[aa][bb]; break;
+          case 2: k = kSymK2[aa][bb]; break;
+          case 3: k = kSymK3[aa][bb]; break;
+          default: k = kSymK4[aa][bb]; break;
+        }
+        if (__builtin_memcmp(&k, &coefs[at + (a + w) * ks + (b + w)], 4) != 0) return false;
+      }
+    at += (size_t)ks * ks;
+  }
+  return true;
+}
+
+// VALU instructions per source row and output column of table width w (the
+// multiplies and adds of the walk plus the accumulator shift).
+static double sym_row_cost(int w) { return (2. * w + 1) * (w + 1) + (2. * w + 1) * (2. * w + 1) + 2. * w + 8; }
+
+// Output rows per wave for each slot.  A wave issues at most one VALU
+// instruction per 4 cycles (two waves per SIMD fill the 2-cycle issue), so a
+// launch cannot end before its longest wave: the widest kernel's chunk is
+// sized so that wave needs at most cp (0.7 for the octaves, measured) of the
+// launch's whole-chip time (a 64 x 1080p octave 0: one 1080-row chunk; 16
+// images per launch, as on one of bench.py's 4 streams: 270-row chunks).
+// Taller chunks recompute less halo (w rows above and below a chunk); the
+// other slots get chunks of about the same work (rows x row cost).
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+static int sym_simds() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+    return 4 * cus;
+  }();
+  return n;
+}
+
+static void sym_plan(SymArgs& A, const int* w, int nslot, double cp) {
+  static const int force = env_int("SIFT_HIP_SYM_ROWS", 0);
+  double total = 0;
+  for (int s = 0; s < nslot; ++s) total += (double)A.strips * A.batch * A.rows * sym_row_cost(w[s]);
+  // longest wave (rows_w0 x cost x 4 cycles) <= cp x whole-chip time (total x 2 cycles / SIMDs)
+  int rows_w0 = (int)(cp * total / (2.0 * sym_simds() * sym_row_cost(w[0])));
+  rows_w0 = force > 0 ? force : std::max(64, rows_w0);
+  const double per = sym_row_cost(w[0]) * rows_w0;
+  int start = 0;
+  for (int s = 0; s < nslot; ++s) {
+    int ch = std::max(1, (int)ceil(A.rows * sym_row_cost(w[s]) / per - 1e-9));
+    const int h = (A.rows + ch - 1) / ch;
+    ch = (A.rows + h - 1) / h;
+    A.chunk[s] = h;
+    A.start[s] = start;
+    start += A.strips * A.batch * ch;
+  }
+  for (int s = nslot; s < 5; ++s) A.start[s] = start;
+}
+
+void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitch, long long dimg, int rows,
+                          int cols, int batch) {
+  SymArgs A{};
+  A.src = src.p;
+  A.s_pitch = src.pitch;
+  A.s_img = src.img_stride;
+  A.dst[0] = dst;
+  A.d_pitch = dpitch;
+  A.d_img = dimg;
+  A.rows = rows;
+  A.cols = cols;
+  A.strips = (cols + 63) / 64;
+  A.batch = batch;
+  const int w[1] = {kSymW0};
+  sym_plan(A, w, 1, 0.35);  // measured: 4 chunks of a 1080p base, not 2
+  hipLaunchKernelGGL(blur_sym_base_kernel, dim3(A.start[1]), dim3(64), 0, st, A);
+}
+
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch) {
+  const Octave& O = L.oct[o];
+  SymArgs A{};
+  A.src = gpyr + O.g_off[0];
+  A.s_pitch = O.pitch;
+  A.s_img = L.g_img;
+  for (int s = 0; s < 4; ++s) A.dst[s] = gpyr + O.g_off[4 - s];
+  A.d_pitch = O.pitch;
+  A.d_img = L.g_img;
+  A.rows = O.rows;
+  A.cols = O.cols;
+  A.strips = (O.cols + 63) / 64;
+  A.batch = batch;
+  const int w[4] = {kSymW4, kSymW3, kSymW2, kSymW1};
+  static const double cp = [] {
+    const char* e = getenv("SIFT_HIP_SYM_CP");
+    return e ? atof(e) : 0.7;
+  }();
+  sym_plan(A, w, 4, cp);
+  hipLaunchKernelGGL(blur_sym_kernel, dim3(A.start[4]), dim3(64), 0, st, A);
 }
 
 // ---- resize INTER_NEAREST to the next octave (src/sift.cpp:252-254) -------

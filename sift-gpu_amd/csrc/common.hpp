@@ -12,11 +12,11 @@
 #include <stdint.h>
 
 #include "../../include/sift_hip.h"
+#include "gauss_host.hpp"
 
 namespace sift {
 
 // ---- tuning constants, src/sift.cpp:4-47 ---------------------------------
-constexpr int kLayers = 2;          // nOctaveLayers
 constexpr int kScales = 5;          // nScales = nOctaveLayers + 3
 constexpr int kDogPer = 4;          // DoG planes per octave
 constexpr int kBorder = 5;          // SIFT_IMG_BORDER
@@ -28,8 +28,6 @@ constexpr int kDescBins = 8;        // SIFT_DESCR_HIST_BINS
 constexpr int kDescLen = 128;
 constexpr int kMaxOctaves = 12;
 constexpr float kDogThreshold = 8.f;  // literal at src/sift.cpp:564
-constexpr double kSigma = 1.6;
-constexpr double kRefPi = 3.14159265359;  // src/sift.cpp:7
 constexpr double kCvPi = 3.1415926535897932384626433832795;
 
 // ---- pyramid layout in HBM ------------------------------------------------
@@ -192,11 +190,17 @@ struct Plane {          // a device plane (or the input image)
 };
 
 // blur.hip
-int gaussian_kernel_host(float sigma, float* coeff);  // src/sift.cpp:95-108
 void launch_blur_plane(hipStream_t st, int w, const float* coef, Plane src, float* dst,
                        long long dpitch, long long dimg, int rows, int cols, int batch);
 void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
                         const int* wsz, int batch);
+// Exact blur in symmetric scatter form for SIFT_NCL's five fixed tables
+// (compile-time constants); sym_tables_match(coefs) checks them against the
+// context's base + octave tables before these are used.
+bool sym_tables_match(const float* coefs);
+void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitch, long long dimg, int rows,
+                          int cols, int batch);
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch);
 void launch_decimate(hipStream_t st, const Layout& L, int o, float* gpyr, int batch);
 void launch_dog(hipStream_t st, const Layout& L, int o, const float* gpyr, float* dog, int batch);
 void launch_blur_1d(hipStream_t st, int w, const float* coef1d, Plane src, float* tmp, float* dst,

@@ -211,6 +211,70 @@ def test_four_octaves_is_prefix_of_five(ctx, oracle):
     assert_bits_equal(desc4, desc5[keep], "descriptors")
 
 
+# ---- scatter-form blur (blur.hip blur_sym_kernel) --------------------------------
+# The library picks the scatter walk for tall planes (>= SIFT_HIP_SYM_ROWS_MIN
+# rows) in launches of >= SIFT_HIP_SYM_MIN strips x images (octave 0 of a
+# 1080p batch) and the 2-D tiles otherwise; these tests force each path (the
+# variables are read when a context is created).
+@pytest.mark.parametrize("shape,b", [((130, 90), 3), ((203, 157), 2), ((300, 421), 9), ((40, 1500), 4),
+                                     ((700, 70), 6)])
+def test_scatter_blur_pyramid_bitexact(siftgpu, oracle, monkeypatch, shape, b):
+    monkeypatch.setenv("SIFT_HIP_SYM_MIN", "0")
+    monkeypatch.setenv("SIFT_HIP_SYM_ROWS_MIN", "0")
+    img = oracle.synth_image(b, *shape)
+    ref = oracle.split_planes(oracle.build_gaussian_pyramid(img), *shape, 5, 5)
+    with siftgpu.Context(*shape, 1, device=0) as c:
+        gp = c.buildGaussianPyramid(img, 5)
+    for i, (p, q) in enumerate(zip(gp, ref)):
+        assert_bits_equal(p, q, f"gpyr plane {i}")
+
+
+@pytest.mark.parametrize("mode", ["sym", "gather"])
+def test_blur_paths_1080p_and_8k_planes(siftgpu, oracle, monkeypatch, mode):
+    """Both blur paths at full size against the CPU path's plane digests: the
+    scatter walk's multi-chunk plans (a 1080p or 8K image is split into
+    chunks per scale) and the 2-D tiles."""
+    monkeypatch.setenv("SIFT_HIP_SYM_MIN", "0" if mode == "sym" else "1000000000")
+    monkeypatch.setenv("SIFT_HIP_SYM_ROWS_MIN", "0")
+    for name, (R, C) in (("synth0_1080x1920", (1080, 1920)), ("synth0_4320x7680", (4320, 7680))):
+        g = load_golden(name)
+        img = oracle.synth_image(0, R, C)
+        with siftgpu.Context(R, C, 1, device=0) as c:
+            gp = c.buildGaussianPyramid(img, 5)
+        assert [sha(p) for p in gp] == list(g["gpyr_sha"]), f"{name} {mode}"
+        del gp
+
+
+def test_scatter_blur_sift_ncl_and_batch(siftgpu, oracle, monkeypatch):
+    import torch
+    monkeypatch.setenv("SIFT_HIP_SYM_MIN", "0")
+    monkeypatch.setenv("SIFT_HIP_SYM_ROWS_MIN", "0")
+    img = oracle.synth_image(9, 480, 640)
+    kps_ref, desc_ref = oracle.sift(img)
+    B, R, C = 3, 240, 320
+    with siftgpu.Context(480, 640, B, device=0) as c:
+        kps, desc = c.SIFT_NCL(img)
+        assert_bits_equal(kp_bytes(kps), kp_bytes(kps_ref), "keypoints")
+        assert_bits_equal(desc, desc_ref, "descriptors")
+        imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
+        c.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=40)
+        cap = 20000
+        kpts = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
+        dsc = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
+        offs = torch.empty((B + 1,), dtype=torch.int32, device="cuda")
+        c.detect_compute_batch(imgs.data_ptr(), B, R, C, C, R * C, kpts.data_ptr(), dsc.data_ptr(), cap,
+                               offs.data_ptr())
+        c.sync()
+        o = offs.cpu().numpy()
+        k = kpts.cpu().numpy().view(np.uint8).reshape(cap, 28)
+        dd = dsc.cpu().numpy()
+    for b in range(B):
+        kr, dr = oracle.sift(oracle.synth_image(40 + b, R, C))
+        assert o[b + 1] - o[b] == len(kr)
+        assert_bits_equal(k[o[b]:o[b + 1]], kp_bytes(kr), f"batch image {b} keypoints")
+        assert_bits_equal(dd[o[b]:o[b + 1]], dr, f"batch image {b} descriptors")
+
+
 # ---- batch mode on device memory -----------------------------------------------
 def test_batch_mode_matches_single(ctx, oracle):
     import torch
