@@ -138,7 +138,7 @@ struct sift_ctx {
   int w_base = 0;
   bool sym_blur = false;          // symmetric scatter blur (blur.hip) for the base and octave scales
   int sym_min = 256;              // ... for launches of >= sym_min 64-column strips x images
-  int sym_rows = 1000;            //     of >= sym_rows rows (a tall plane: little halo per chunk)
+  int sym_rows = 0;               //     of >= sym_rows rows (A/B knob, SIFT_HIP_SYM_ROWS_MIN)
   size_t coef_base_off = 0, coef_oct_off = 0;
   MathConsts* d_mc = nullptr;
   DetectBufs D{};
@@ -613,7 +613,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     c->sym_blur = sym_tables_match(coefs.data()) && !(e && atoi(e) != 0);
     // a scatter walk is a tall column strip (its halo is recomputed per
     // chunk), so it needs many strips to fill the chip; small launches (one
-    // 1080p image) keep the 2-D tiles.  SIFT_HIP_SYM_MIN=0 forces it (tests).
+    // 1080p or 8K image, the last octaves of a batch) keep the 2-D tiles.
+    // SIFT_HIP_SYM_MIN=0 forces it (tests).
     const char* m = getenv("SIFT_HIP_SYM_MIN");
     if (m) c->sym_min = atoi(m);
     const char* r = getenv("SIFT_HIP_SYM_ROWS_MIN");

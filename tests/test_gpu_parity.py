@@ -212,10 +212,10 @@ def test_four_octaves_is_prefix_of_five(ctx, oracle):
 
 
 # ---- scatter-form blur (blur.hip blur_sym_kernel) --------------------------------
-# The library picks the scatter walk for tall planes (>= SIFT_HIP_SYM_ROWS_MIN
-# rows) in launches of >= SIFT_HIP_SYM_MIN strips x images (octave 0 of a
-# 1080p batch) and the 2-D tiles otherwise; these tests force each path (the
-# variables are read when a context is created).
+# The library picks the scatter walk for launches of >= SIFT_HIP_SYM_MIN
+# (256) 64-column strips x images (octaves 0-3 of a 64 x 1080p batch) and the
+# 2-D tiles otherwise; these tests force each path (the variables are read
+# when a context is created).
 @pytest.mark.parametrize("shape,b", [((130, 90), 3), ((203, 157), 2), ((300, 421), 9), ((40, 1500), 4),
                                      ((700, 70), 6)])
 def test_scatter_blur_pyramid_bitexact(siftgpu, oracle, monkeypatch, shape, b):

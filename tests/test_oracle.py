@@ -3,11 +3,12 @@ restates is checked against an independent numpy/double re-derivation, the
 whole path against the committed golden fixtures, plus size-independent
 properties.  PARITY UNPINNED vs the real reference (see sift_oracle.h)."""
 import math
+import os
 
 import numpy as np
 import pytest
 
-from conftest import book_image, kp_bytes, load_golden, sha
+from conftest import ROOT, book_image, kp_bytes, load_golden, sha
 
 PI_REF = 3.14159265359          # src/sift.cpp:7
 PYR_SIGMAS = [math.sqrt(1.6 * 1.6 + 0.2 * 0.2)] + [
@@ -59,6 +60,29 @@ def np_exp32f(x):
     sc = (t << 23).view(np.float32)
     poly = (((v + A1) * v + A2) * v + A3) * v + A4
     return (sc * tab[vi & 63]) * poly
+
+
+def test_scatter_blur_tables_match_oracle(oracle, tmp_path):
+    """The compile-time tables of the scatter-form blur (blur.hip,
+    build/sym_coefs.inc, printed by csrc/gen_sym_coefs.cpp) against the
+    oracle's getGaussianKernel for the same sigmas: every quadrant entry
+    K[|a|][|b|], bit for bit, and the five SIFT_NCL widths."""
+    import re
+    import subprocess
+    src = os.path.join(ROOT, "sift-gpu_amd", "csrc", "gen_sym_coefs.cpp")
+    exe = str(tmp_path / "gen")
+    subprocess.run(["g++", "-O0", "-fno-builtin", "-std=c++17", "-o", exe, src, "-lm"], check=True)
+    text = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
+    tables = re.findall(r"constexpr int kSymW(\d) = (\d+);  // sigma (\S+)\nconstexpr float kSymK\d\[\d+\]\[\d+\] = "
+                        r"\{\n(.*?)\n\};", text, re.S)
+    assert [int(t[1]) for t in tables] == [4, 4, 8, 12, 18]
+    for _, w, sig, body in tables:
+        w = int(w)
+        got = np.array([float.fromhex(v.rstrip("f")) for v in re.findall(r"-?0x[0-9a-fp.+-]+f", body)],
+                       np.float32).reshape(w + 1, w + 1)
+        ref = oracle.gaussian_kernel(float.fromhex(sig))
+        assert ref.shape == (2 * w + 1, 2 * w + 1)
+        np.testing.assert_array_equal(got.view(np.uint32), ref[w:, w:].view(np.uint32))
 
 
 def test_exp32f(oracle):
