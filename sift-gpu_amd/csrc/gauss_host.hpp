@@ -34,6 +34,19 @@ inline int gaussian_kernel_host(float sigma, float* coeff) {
   return size;
 }
 
+// SIFT_FLAG_FAST's 1-D taps: g(a) = exp(-a^2 / (2 sigma^2)) / sqrt(2 pi sigma^2)
+// for a in [-w, w], the square root of getGaussianKernel's normalisation
+// (src/sift.cpp:103, same float 2*sigma*sigma chain and PI), so that
+// K[a][b] / 8192 = g(a) g(b) up to float rounding.  Returns 2w+1.
+inline int fast_taps_host(float sigma, float* g) {
+  const int w = (int)floor(3 * sigma);
+  const double den = (double)(2 * sigma * sigma);
+  const double nrm = 1. / sqrt(2 * kRefPi * sigma * sigma);
+  if (g)
+    for (int a = -w; a <= w; ++a) g[a + w] = (float)(nrm * exp(-(a * a) * 1. / den));
+  return 2 * w + 1;
+}
+
 // The five blur sigmas of SIFT_NCL: the base sqrt(1.6^2 + 0.2^2)
 // (src/sift.cpp:237) and sig[1..4] (:240-245).
 inline void sift_sigmas(float* base, float* sig) {

@@ -629,15 +629,7 @@ __global__ __launch_bounds__(256, 2) void pyr_fast_kernel(FastArgs A) {
 
 #undef SIFT_VM_WAIT
 
-// 1-D taps of sigma: g(a) = exp(-a^2 / (2 sigma^2)) / sqrt(2 pi sigma^2), the
-// square root of the 2-D kernel's normalisation (src/sift.cpp:103, same
-// float 2*sigma*sigma chain and PI).
-void fast_taps(float sigma, float* g) {
-  const int w = (int)floor(3 * sigma);
-  const double den = (double)(2 * sigma * sigma);
-  const double nrm = 1. / sqrt(2 * kRefPi * sigma * sigma);
-  for (int a = -w; a <= w; ++a) g[a + w] = (float)(nrm * exp(-(a * a) * 1. / den));
-}
+void fast_taps(float sigma, float* g) { fast_taps_host(sigma, g); }
 
 }  // namespace
 
