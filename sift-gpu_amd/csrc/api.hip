@@ -139,7 +139,6 @@ struct sift_ctx {
   bool sym_blur = false;          // symmetric scatter blur (blur.hip) for the base and octave scales
   int sym_min = 256;              // ... for launches of >= sym_min 64-column strips x images
   int sym_rows = 0;               //     of >= sym_rows rows (A/B knob, SIFT_HIP_SYM_ROWS_MIN)
-  bool fast_walk = true;          // SIFT_FLAG_FAST: column walks (pyramid_walk.hip), else pyramid_fast.hip
   size_t coef_base_off = 0, coef_oct_off = 0;
   MathConsts* d_mc = nullptr;
   DetectBufs D{};
@@ -317,10 +316,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       const double px = plane_px(L, o) * batch;
       const double taps = 2.0 * (9 + 17 + 25 + 37) + (o == 0 ? 2.0 * 9 : 0.0);
       StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-      if (c->fast_walk)
-        launch_pyramid_walk(st, L, o, c->d_gpyr, src, batch);
-      else
-        launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
+      launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
     }
     if (with_dog)
       for (int o = 0; o < L.n_oct; ++o) {
@@ -623,8 +619,6 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     if (m) c->sym_min = atoi(m);
     const char* r = getenv("SIFT_HIP_SYM_ROWS_MIN");
     if (r) c->sym_rows = atoi(r);
-    const char* f = getenv("SIFT_HIP_FAST_V1");
-    c->fast_walk = !(f && atoi(f) != 0);
   }
   c->fast_taps.resize(fast_coefs_size());
   if (fast_coefs_host(sb, sig_f, c->fast_taps.data()) != 0) return bail(SIFT_E_INVALID);

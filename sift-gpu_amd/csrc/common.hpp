@@ -224,8 +224,6 @@ void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int n
                    float2* part_d, int2* part_i, int* idx, float* dist);
 void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
                          const void* coef);
-// pyramid_walk.hip: the same pyramid as independent column walks (default)
-void launch_pyramid_walk(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
 
 // detect.hip
 struct DetectBufs {
