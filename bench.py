@@ -9,7 +9,7 @@ BASELINE.json configs[2] at N=1; at N=8 the 8 x 64 = 512 images are
 configs[3]).  Inputs are generated on device (integer-exact generator,
 SURVEY.md 8(d) d2) before the timed region; every rank has its own images
 (weak scaling).  The timed step runs the per-GPU batch as --streams (default
-4) sub-batches, one library context and HIP stream each, with no
+2) sub-batches, one library context and HIP stream each, with no
 synchronisation between them inside the timed region (graph replay; the
 streams' stages overlap).  For N > 1 each sub-batch's keypoints are gathered
 to rank 0 over RCCL one step behind the compute (sift-gpu_amd/sift_dist.py),
@@ -71,7 +71,7 @@ def parse():
     p.add_argument("--no-fast", action="store_true", help="skip the SIFT_FLAG_FAST leg")
     p.add_argument("--no-match", action="store_true", help="skip the knnMatch leg (SURVEY 8(f) f2)")
     p.add_argument("--no-single", action="store_true", help="skip the configs[1] single-image leg")
-    p.add_argument("--streams", type=int, default=4,
+    p.add_argument("--streams", type=int, default=2,
                    help="timed legs: the per-GPU batch as this many sub-batches, one context + HIP stream each")
     p.add_argument("--no-8k", action="store_true", help="skip the configs[4] 7680x4320 leg")
     p.add_argument("--only", default=None, choices=[None, "exact", "fast", "single", "8k"],

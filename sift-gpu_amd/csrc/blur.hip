@@ -421,8 +421,14 @@ __device__ __forceinline__ void sym_walk(const SymArgs& A, int slot, int local, 
 
 // Waves are independent (one 64-lane workgroup each).  The octave kernel's
 // slots run in launch order, widest kernel first: slot s blurs scale 4 - s.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void blur_sym_kernel(SymArgs A) {
+// OCC = 3 (default): the kernel holds 168 VGPRs, 3 waves per SIMD instead of
+// the 4 its 101 allow.  Alone it runs as fast (3 waves keep the 2-cycle VALU
+// issue full); beside another stream's latency-bound kernels (bench.py's 2
+// streams) the step is 3-4 % shorter, measured (SIFT_HIP_SYM_OCC=4 restores 4).
+template <int OCC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void blur_sym_kernel(SymArgs A) {
   __shared__ float ring[kSymRing];
+  if constexpr (OCC == 3) asm volatile("; hold v160-v167" ::: "v160", "v167");
   const int wid = blockIdx.x;
   const int slot = wid >= A.start[3] ? 3 : wid >= A.start[2] ? 2 : wid >= A.start[1] ? 1 : 0;
   const int local = wid - A.start[slot];
@@ -549,7 +555,11 @@ void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr,
     return e ? atof(e) : 0.7;
   }();
   sym_plan(A, w, 4, cp);
-  hipLaunchKernelGGL(blur_sym_kernel, dim3(A.start[4]), dim3(64), 0, st, A);
+  static const int occ = env_int("SIFT_HIP_SYM_OCC", 3);
+  if (occ == 4)
+    hipLaunchKernelGGL(blur_sym_kernel<4>, dim3(A.start[4]), dim3(64), 0, st, A);
+  else
+    hipLaunchKernelGGL(blur_sym_kernel<3>, dim3(A.start[4]), dim3(64), 0, st, A);
 }
 
 // ---- resize INTER_NEAREST to the next octave (src/sift.cpp:252-254) -------
