@@ -230,6 +230,228 @@ __global__ __launch_bounds__(256) void dog_extrema_kernel(TileArgs A) {
   }
 }
 
+// ---- pass 1, walking form (default) -----------------------------------------
+// One wave owns a 64-column strip (64-aligned, so its ballots are exactly two
+// mask words per row) of one octave and walks a chunk of rows.  Each row of
+// the five Gaussian planes (or the caller's DoG planes) is loaded once --
+// lanes 0 and 1 also fetch the columns x0-1 and x0+64 -- one row ahead of its
+// use, turned into the four DoG rows + Gaussian layers 1, 2 and put into a
+// three-row LDS ring; row y is then tested and its gradients written as soon
+// as row y+1 is in the ring.  Against the 64x16 tiles above: no 2-row halo
+// per tile (rows are read once per chunk), the loads of the next row fly
+// while the current one is tested, and a wave needs 4.9 KB of LDS instead of
+// a quarter of 29 KB, so 8 waves per SIMD stay resident.  Same values, same
+// bits (the 26-neighbour test only compares; the gradients and DoG are the
+// same float expressions).
+constexpr int kWCols = 64 + 4;  // ring row: column x0 - 1 + c at c (c = 0..65)
+
+struct WalkArgs {
+  Layout L;
+  MaskLayout M;
+  const float* gpyr;
+  const float* dog;
+  float2* grad;
+  const MathConsts* mc;
+  unsigned* mask;
+  int wave_start[kMaxOctaves + 1];  // first wave (blockIdx.x) of octave o
+  int strips[kMaxOctaves];
+  int chunk;                        // rows per wave
+};
+
+// src/sift.cpp:493-511 at ring column c: lo/cu/hi[k] = row y - 1 + k of the
+// layer below / at / above the tested one; ties pass.
+__device__ __forceinline__ bool ring_extremum(const float* const (&lo)[3], const float* const (&cu)[3],
+                                              const float* const (&hi)[3], int c) {
+  const float v = cu[1][c];
+  if (!(fabsf(v) > kDogThreshold)) return false;
+  bool ok = true;
+  if (v > 0) {
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        ok = ok && v >= lo[dy][c + dx] && v >= hi[dy][c + dx];
+        if (dy != 1 || dx != 0) ok = ok && v >= cu[dy][c + dx];
+      }
+  } else if (v < 0) {
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        ok = ok && v <= lo[dy][c + dx] && v <= hi[dy][c + dx];
+        if (dy != 1 || dx != 0) ok = ok && v <= cu[dy][c + dx];
+      }
+  } else {
+    ok = false;
+  }
+  return ok;
+}
+
+template <bool FROM_G>
+__global__ __launch_bounds__(64) void extrema_walk_kernel(WalkArgs A) {
+  __shared__ float ring[3][6][kWCols];  // planes: DoG 0..3, Gaussian layers 1, 2
+  const int lane = threadIdx.x;
+  const int b = blockIdx.y;
+  const int t = blockIdx.x;
+  int o = 0;
+  while (o + 1 < A.L.n_oct && A.wave_start[o + 1] <= t) ++o;
+  const int local = t - A.wave_start[o];
+  const Octave& O = A.L.oct[o];
+  const int x0 = (local % A.strips[o]) * 64, y0 = (local / A.strips[o]) * A.chunk;
+  const int y1 = min(y0 + A.chunk, O.rows);
+  const int rows = O.rows, cols = O.cols;
+  const long long pitch = O.pitch;
+  const float* g = A.gpyr + b * A.L.g_img;
+  const float* dg = FROM_G ? nullptr : A.dog + b * A.L.d_img;
+  const int xm = x0 + lane;                       // this lane's column
+  const int xh = lane == 0 ? x0 - 1 : x0 + 64;    // halo column of lanes 0, 1
+  const bool hl = lane < 2;
+  const int xmc = min(xm, cols - 1), xhc = min(max(xh, 0), cols - 1);
+  // loads of row r (clamped addresses; out-of-image values are zeroed when the
+  // row is put): G1, G2 and then G0, G3, G4 (FROM_G) or the DoG planes 0..3
+  auto load = [&](int r, float (&v)[6], float (&h)[6]) {
+    const long long rp = (long long)min(max(r, 0), rows - 1) * pitch;
+    const long long pm = rp + xmc, ph = rp + xhc;
+    v[0] = g[O.g_off[1] + pm];
+    v[1] = g[O.g_off[2] + pm];
+    if (FROM_G) {
+      v[2] = g[O.g_off[0] + pm];
+      v[3] = g[O.g_off[3] + pm];
+      v[4] = g[O.g_off[4] + pm];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kDogPer; ++k) v[2 + k] = dg[O.d_off[k] + pm];
+    }
+    if (hl) {
+      h[0] = g[O.g_off[1] + ph];
+      h[1] = g[O.g_off[2] + ph];
+      if (FROM_G) {
+        h[2] = g[O.g_off[0] + ph];
+        h[3] = g[O.g_off[3] + ph];
+        h[4] = g[O.g_off[4] + ph];
+      } else {
+#pragma unroll
+        for (int k = 0; k < kDogPer; ++k) h[2 + k] = dg[O.d_off[k] + ph];
+      }
+    }
+  };
+  // DoG (src/sift.cpp:280: dog = g[i+1] - g[i]) and the Gaussian layers into
+  // ring slot s at column c; 0 outside the image, as the tile kernel
+  // the lane's own column of the ring, kept in registers as well: od[slot][k]
+  // = DoG plane k, og[slot][l] = Gaussian layer 1 + l (slots are compile-time
+  // constants in the unrolled walk below)
+  float od[3][kDogPer], og[3][2];
+  auto put1 = [&](int s, int c, const float (&v)[6], bool ok, float (&d)[kDogPer], float (&gg)[2]) {
+    const float g1 = ok ? v[0] : 0.f, g2 = ok ? v[1] : 0.f;
+    if (FROM_G) {
+      const float g0 = ok ? v[2] : 0.f, g3 = ok ? v[3] : 0.f, g4 = ok ? v[4] : 0.f;
+      d[0] = g1 - g0;
+      d[1] = g2 - g1;
+      d[2] = g3 - g2;
+      d[3] = g4 - g3;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kDogPer; ++k) d[k] = ok ? v[2 + k] : 0.f;
+    }
+    gg[0] = g1;
+    gg[1] = g2;
+#pragma unroll
+    for (int k = 0; k < kDogPer; ++k) ring[s][k][c] = d[k];
+    ring[s][4][c] = g1;
+    ring[s][5][c] = g2;
+  };
+  auto put = [&](int s, int r, const float (&v)[6], const float (&h)[6]) {
+    const bool rok = r >= 0 && r < rows;
+    put1(s, lane + 1, v, rok && xm < cols, od[s], og[s]);
+    if (hl) {
+      float dh[kDogPer], gh[2];
+      put1(s, lane == 0 ? 0 : 65, h, rok && xh >= 0 && xh < cols, dh, gh);
+    }
+  };
+  const AtanConsts ak = A.mc->t;
+  float2* gr = A.grad + b * A.L.g_img;
+  const int wpr = A.M.wpr[2 * o];
+  const long long mbase = b * A.M.w_img;
+  // row y from ring slots su (y-1), sm (y), sd (y+1)
+  auto process = [&](int y, int su, int sm, int sd) {
+    const int c = lane + 1;
+    if (y > 0 && y < rows - 1 && xm > 0 && xm < cols - 1) {
+#pragma unroll
+      for (int ls = 0; ls < 2; ++ls) {
+        const float dx = (float)(ring[sm][4 + ls][c + 1] - ring[sm][4 + ls][c - 1]);
+        const float dy = (float)(og[su][ls] - og[sd][ls]);
+        gr[O.g_off[1 + ls] + (long long)y * pitch + xm] = make_float2(magnitude(dx, dy), fast_atan2(dy, dx, ak));
+      }
+    }
+    // src/sift.cpp:493-511, both detection layers: v at (y, x) of DoG plane
+    // 1 (layer 1) / 2 (layer 2) is an extremum when |v| > 8 and v >= (<=)
+    // all 26 neighbours -- ties pass -- i.e. v >= the max (v <= the min) of
+    // the neighbours (finite values: the order of the comparisons does not
+    // matter).  Branch-free: per plane the max / min of the 3x3 block,
+    // without its centre for the two planes whose centres are tested.
+    const int s3[3] = {su, sm, sd};
+    float mx9[kDogPer], mn9[kDogPer], mx8[2], mn8[2];
+#pragma unroll
+    for (int k = 0; k < kDogPer; ++k) {
+      float l3[3], r3[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        l3[dy] = ring[s3[dy]][k][c - 1];
+        r3[dy] = ring[s3[dy]][k][c + 1];
+      }
+      const float own_ud_max = fmaxf(od[su][k], od[sd][k]), own_ud_min = fminf(od[su][k], od[sd][k]);
+      const float side_max = fmaxf(fmaxf(fmaxf(l3[0], l3[1]), l3[2]), fmaxf(fmaxf(r3[0], r3[1]), r3[2]));
+      const float side_min = fminf(fminf(fminf(l3[0], l3[1]), l3[2]), fminf(fminf(r3[0], r3[1]), r3[2]));
+      const float m8x = fmaxf(side_max, own_ud_max), m8n = fminf(side_min, own_ud_min);
+      mx9[k] = fmaxf(m8x, od[sm][k]);
+      mn9[k] = fminf(m8n, od[sm][k]);
+      if (k == 1 || k == 2) {
+        mx8[k - 1] = m8x;
+        mn8[k - 1] = m8n;
+      }
+    }
+    const bool inside = y >= kBorder && y < rows - kBorder && xm >= kBorder && xm < cols - kBorder;
+    bool f[2];
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const float v = od[sm][1 + l];
+      const float nmax = fmaxf(fmaxf(mx9[l], mx8[l]), mx9[l + 2]);
+      const float nmin = fminf(fminf(mn9[l], mn8[l]), mn9[l + 2]);
+      f[l] = inside && fabsf(v) > kDogThreshold && ((v > 0 && v >= nmax) || (v < 0 && v <= nmin));
+    }
+    const unsigned long long m1 = __ballot(f[0]), m2 = __ballot(f[1]);
+    if (lane == 0 || lane == 32) {
+      const int w = x0 / 32 + (lane >> 5);
+      if (w < wpr) {
+        const long long base = mbase + (long long)y * wpr + w;
+        A.mask[base + A.M.start[2 * o]] = (unsigned)(m1 >> lane);
+        A.mask[base + A.M.start[2 * o + 1]] = (unsigned)(m2 >> lane);
+      }
+    }
+  };
+  // rows y0-1 .. y1 enter the ring in order (row y0-1+i in slot i % 3); row y
+  // is processed once row y+1 is in.  Three register sets rotate, so the
+  // loads of the next two rows are in flight while a row is processed.
+  float va[6], ha[6], vb[6], hb[6], vc[6], hc[6];
+  load(y0 - 1, va, ha);
+  load(y0, vb, hb);
+  load(y0 + 1, vc, hc);
+  // ring slot of row r: (r - y0 + 1) % 3, i.e. set a <-> slot 0, b <-> 1, c <-> 2
+  auto step = [&](int r, float (&v)[6], float (&h)[6], int sr) {
+    put(sr, r, v, h);
+    wave_sync();
+    if (r + 3 <= y1) load(r + 3, v, h);
+    if (r >= y0 + 1) process(r - 1, (sr + 1) % 3, (sr + 2) % 3, sr);
+  };
+  for (int r = y0 - 1; r <= y1; r += 3) {
+    step(r, va, ha, 0);
+    if (r + 1 > y1) break;
+    step(r + 1, vb, hb, 1);
+    if (r + 2 > y1) break;
+    step(r + 2, vc, hc, 2);
+  }
+}
+
 // ---- pass 2: ordered compaction of the bitmask ----------------------------
 __global__ __launch_bounds__(256) void mask_count_kernel(const unsigned* __restrict__ mask, long long w_img,
                                                          int bpw, int* __restrict__ blk_counts) {
@@ -475,7 +697,38 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
     t += A.tiles_x[o] * ((L.oct[o].rows + kExTH - 1) / kExTH);
   }
   A.tile_start[L.n_oct] = t;
-  hipLaunchKernelGGL(dog_extrema_kernel, dim3(t, batch), dim3(256), 0, st, A);
+  static const bool tiles = [] {
+    const char* e = getenv("SIFT_HIP_EXTREMA_TILES");  // A/B switch: the 64x16 tile kernel
+    return e && atoi(e) != 0;
+  }();
+  if (tiles) {
+    hipLaunchKernelGGL(dog_extrema_kernel, dim3(t, batch), dim3(256), 0, st, A);
+  } else {
+    WalkArgs W;
+    W.L = L;
+    W.M = A.M;
+    W.gpyr = gpyr;
+    W.dog = dog;
+    W.grad = grad;
+    W.mc = mc;
+    W.mask = D.mask;
+    // rows per wave: about 16 K waves over the launch (8 per SIMD, two rounds),
+    // at least 8 rows (a chunk re-reads 2 rows)
+    long long strip_rows = 0;
+    for (int o = 0; o < L.n_oct; ++o) strip_rows += (long long)((L.oct[o].cols + 63) / 64) * L.oct[o].rows;
+    W.chunk = (int)std::min<long long>(512, std::max<long long>(8, strip_rows * batch / 16384));
+    int w = 0;
+    for (int o = 0; o < L.n_oct; ++o) {
+      W.wave_start[o] = w;
+      W.strips[o] = (L.oct[o].cols + 63) / 64;
+      w += W.strips[o] * ((L.oct[o].rows + W.chunk - 1) / W.chunk);
+    }
+    W.wave_start[L.n_oct] = w;
+    if (write_dog)
+      hipLaunchKernelGGL(extrema_walk_kernel<true>, dim3(w, batch), dim3(64), 0, st, W);
+    else
+      hipLaunchKernelGGL(extrema_walk_kernel<false>, dim3(w, batch), dim3(64), 0, st, W);
+  }
   const MaskLayout& M = A.M;
   hipLaunchKernelGGL(mask_count_kernel, dim3(M.bpw, batch), dim3(256), 0, st, D.mask, M.w_img, M.bpw,
                      D.blk_counts);
