@@ -712,11 +712,17 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
     W.grad = grad;
     W.mc = mc;
     W.mask = D.mask;
-    // rows per wave: about 16 K waves over the launch (8 per SIMD, two rounds),
-    // at least 8 rows (a chunk re-reads 2 rows)
+    // rows per wave: about 64 K waves over the launch (measured on the
+    // 64 x 1080p batch: 16 K 1.70 ms, 32 K 1.60, 64 K 1.56), at least 8 rows
+    // (a chunk re-reads 2 rows)
     long long strip_rows = 0;
     for (int o = 0; o < L.n_oct; ++o) strip_rows += (long long)((L.oct[o].cols + 63) / 64) * L.oct[o].rows;
-    W.chunk = (int)std::min<long long>(512, std::max<long long>(8, strip_rows * batch / 16384));
+    static const long long target = [] {
+      const char* e = getenv("SIFT_HIP_EXTREMA_WAVES");  // tuning knob (A/B runs)
+      const long long v = e ? atoll(e) : 65536;
+      return v > 0 ? v : 65536;
+    }();
+    W.chunk = (int)std::min<long long>(512, std::max<long long>(8, strip_rows * batch / target));
     int w = 0;
     for (int o = 0; o < L.n_oct; ++o) {
       W.wave_start[o] = w;
