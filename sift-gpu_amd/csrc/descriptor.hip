@@ -26,6 +26,9 @@
 #include "common.hpp"
 
 #include <float.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 namespace sift {
 
@@ -72,12 +75,36 @@ __device__ __forceinline__ void slab(float a, float b, int& lo, int& hi) {
   hi = min(hi, (int)fminf(floorf(x1), 1e6f));
 }
 
-__global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
+// Record hand-off, two forms (same sums, same bits):
+//   PACKED = false: records (qidx, value) as float2 at [sample][group][owner]
+//     (4.2 KB), a 32-bit row table (2.6 KB): 12.4 KB of LDS per wave;
+//   PACKED = true: values at [group][owner][sample] (2.1 KB, the owner reads
+//     its 8 values with two ds_read_b128), bin bytes at [group][owner][sample]
+//     (0.5 KB, one ds_read_b64), a 16-bit row table (1.3 KB): 9.4 KB per
+//     wave, and the in-flight records packed as 8 values + 2 words of bin
+//     bytes, so four waves per SIMD fit instead of three.
+constexpr int kRecG = 68;  // PACKED value words per group (8 owners x 8 samples + pad: b128 reads conflict free)
+
+template <bool PACKED>
+struct RecT {  // one lane's 8 corner records: (qidx, value) pairs
+  float4 r[4];
+};
+template <>
+struct RecT<true> {
+  float v[8];
+  unsigned qb[2];  // qidx of corner k in byte k & 3 of word k >> 2
+};
+
+template <bool PACKED>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 : 1))) void descriptor_kernel(
+    DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
-  // per-sample hand-off records: [sample j][group][owner q] = (bin qidx, value),
-  // row stride kRecStride2 words
-  __shared__ __attribute__((aligned(16))) float rec[8 * kRecStride2];
-  __shared__ int rows_tab[kGrp][kMaxWinRows];       // per row: (jlo + 64) | len << 16
+  // per-sample hand-off records (see RecT)
+  __shared__ __attribute__((aligned(16))) float rec[PACKED ? kGrp * kRecG : 8 * kRecStride2];
+  __shared__ __attribute__((aligned(16))) unsigned char recq[PACKED ? 64 * 8 : 16];
+  // per row: (jlo + 64) | len << 16 (PACKED: << 8, 16 bits)
+  __shared__ typename std::conditional<PACKED, unsigned short, int>::type rows_tab[kGrp][kMaxWinRows];
+  constexpr int kLenSh = PACKED ? 8 : 16, kLoMask = PACKED ? 0xff : 0xffff;
   __shared__ float bc[kGrp][4];
   __shared__ int sord[kGrp];                        // this sub-batch's keypoint indices
   const int lane = threadIdx.x & 63;
@@ -177,7 +204,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
         slab(sin_t, i * cos_t, lo, hi);     // r_rot = j*sin_t + i*cos_t
         slab(cos_t, -(i * sin_t), lo, hi);  // c_rot = j*cos_t - i*sin_t
         const int len = hi >= lo ? hi - lo + 1 : 0;
-        rows_tab[g][ri] = len ? (lo + 64) | (len << 16) : 0;  // lo in [-40, 40] when len > 0
+        rows_tab[g][ri] = len ? (lo + 64) | (len << kLenSh) : 0;  // lo in [-40, 40] when len > 0
         nsamp += len;
       }
       nsamp += __shfl_xor(nsamp, 1);
@@ -196,15 +223,15 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
     int ri = 0, u = q, rlo = -radius, rlen = D;
     if (table && D > 0) {
       const int e = rows_tab[g][0];
-      rlo = (e & 0xffff) - 64;
-      rlen = e >> 16;
+      rlo = (e & kLoMask) - 64;
+      rlen = e >> kLenSh;
     }
     while (ri < D && u >= rlen) {
       u -= rlen;
       if (++ri < D && table) {
         const int e = rows_tab[g][ri];
-        rlo = (e & 0xffff) - 64;
-        rlen = e >> 16;
+        rlo = (e & kLoMask) - 64;
+        rlen = e >> kLenSh;
       }
     }
     // Software pipeline: each step stashes batch k, then computes batch k+1
@@ -222,8 +249,8 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
     // or in the trash row when Rm+dr or Cm+dc leaves [0, 4).
     // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
     // the owner adds its lane to form the [qidx][lane] address.
-    float4 rc_cur[4];  // (qidx, val) x 8 corners of this lane's sample
-    auto sample = [&](bool in_range, float4 (&out)[4], int& odd_out) {
+    RecT<PACKED> rc_cur;  // (qidx, val) x 8 corners of this lane's sample
+    auto sample = [&](bool in_range, RecT<PACKED>& out, int& odd_out) {
       const int i = ri - radius, j = rlo + u;
       const float c_rot = j * cos_t - i * sin_t;
       const float r_rot = j * sin_t + i * cos_t;
@@ -271,10 +298,17 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
                          r0v && c1v ? q2 : kTrash,       r0v && c1v ? q2 + a1 : kTrash,
                          r1v && c0v ? q4 : kTrash,       r1v && c0v ? q4 + a1 : kTrash,
                          r1v && c1v ? q4 + a5 : kTrash,  r1v && c1v ? q4 + a5 + a1 : kTrash};
+      if constexpr (PACKED) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        out[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
-                             v[2 * t + 1]);
+        for (int k = 0; k < 8; ++k) out.v[k] = v[k];
+        out.qb[0] = qk[0] | (qk[1] << 8) | (qk[2] << 16) | (qk[3] << 24);
+        out.qb[1] = qk[4] | (qk[5] << 8) | (qk[6] << 16) | (qk[7] << 24);
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          out.r[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
+                                 v[2 * t + 1]);
+      }
       odd_out = odd;
     };
     // Entry ri+1 of the row table rides in a register (loaded one advance
@@ -288,16 +322,16 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       u = mv ? u - rlen : u;
       ri = mv ? ri + 1 : ri;
       if (table) {
-        rlo = mv ? (enext & 0xffff) - 64 : rlo;
-        rlen = mv ? enext >> 16 : rlen;
+        rlo = mv ? (enext & kLoMask) - 64 : rlo;
+        rlen = mv ? enext >> kLenSh : rlen;
       }
       if (__builtin_amdgcn_ballot_w64(ri < D && u >= rlen) != 0) {
         while (ri < D && u >= rlen) {
           u -= rlen;
           if (++ri < D && table) {
             const int e = rows_tab[g][ri];
-            rlo = (e & 0xffff) - 64;
-            rlen = e >> 16;
+            rlo = (e & kLoMask) - 64;
+            rlen = e >> kLenSh;
           }
         }
       }
@@ -309,27 +343,51 @@ __global__ __launch_bounds__(64) void descriptor_kernel(DescArgs A) {
       advance();
     }
     for (int base = 0; base < nmax; base += 8) {
-      float2* dst2 = reinterpret_cast<float2*>(rec + q * kRecStride2 + g * 16);
+      if constexpr (PACKED) {
+        // corner k to owner slot s = k ^ odd: value at [g][s][q], bin byte at [g][s][q]
+        float* dv = rec + g * kRecG + q;
+        unsigned char* dq = recq + g * 64 + q;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        dst2[(2 * t) ^ odd_cur] = make_float2(rc_cur[t].x, rc_cur[t].y);
-        dst2[(2 * t + 1) ^ odd_cur] = make_float2(rc_cur[t].z, rc_cur[t].w);
+        for (int k = 0; k < 8; ++k) {
+          const int sl = (k ^ odd_cur) * 8;
+          dv[sl] = rc_cur.v[k];
+          dq[sl] = (unsigned char)(rc_cur.qb[k >> 2] >> (8 * (k & 3)));
+        }
+      } else {
+        float2* dst2 = reinterpret_cast<float2*>(rec + q * kRecStride2 + g * 16);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          dst2[(2 * t) ^ odd_cur] = make_float2(rc_cur.r[t].x, rc_cur.r[t].y);
+          dst2[(2 * t + 1) ^ odd_cur] = make_float2(rc_cur.r[t].z, rc_cur.r[t].w);
+        }
       }
       wave_sync_d();
-      float4 rc_nxt[4];
+      RecT<PACKED> rc_nxt;
       int odd_nxt = 0;
       sample(base + 8 + q < nsamp, rc_nxt, odd_nxt);
       // ordered accumulation of batch k: lane q applies its record of each sample
+      if constexpr (PACKED) {
+        const float4* sv = reinterpret_cast<const float4*>(rec + g * kRecG + q * 8);
+        const float4 va = sv[0], vb = sv[1];
+        const uint2 qq = *reinterpret_cast<const uint2*>(recq + lane * 8);
+        const float vals[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const float2 e = reinterpret_cast<const float2*>(rec + jj * kRecStride2)[lane];
-        const int a = (__float_as_int(e.x) << 6) + lane;
-        hist[a] = hist[a] + e.y;
+        for (int jj = 0; jj < 8; ++jj) {
+          const int qi = ((jj < 4 ? qq.x : qq.y) >> (8 * (jj & 3))) & 0xff;
+          const int a = (qi << 6) + lane;
+          hist[a] = hist[a] + vals[jj];
+        }
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const float2 e = reinterpret_cast<const float2*>(rec + jj * kRecStride2)[lane];
+          const int a = (__float_as_int(e.x) << 6) + lane;
+          hist[a] = hist[a] + e.y;
+        }
       }
       wave_sync_d();
       advance();
-#pragma unroll
-      for (int t = 0; t < 4; ++t) rc_cur[t] = rc_nxt[t];
+      rc_cur = rc_nxt;
       odd_cur = odd_nxt;
     }
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
@@ -437,8 +495,16 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
   A.desc = desc;
   A.first_octave = first_octave;
   A.err_flag = err_flag;
-  hipLaunchKernelGGL(descriptor_kernel, dim3(resident_grid((const void*)descriptor_kernel, 64, 0, 8192)), dim3(64), 0,
-                     st, A);
+  static const bool packed = [] {
+    const char* e = getenv("SIFT_HIP_DESC_PACKED");  // A/B switch between the two record forms
+    return !e || atoi(e) != 0;
+  }();
+  if (packed)
+    hipLaunchKernelGGL(descriptor_kernel<true>, dim3(resident_grid((const void*)descriptor_kernel<true>, 64, 0, 8192)),
+                       dim3(64), 0, st, A);
+  else
+    hipLaunchKernelGGL(descriptor_kernel<false>,
+                       dim3(resident_grid((const void*)descriptor_kernel<false>, 64, 0, 8192)), dim3(64), 0, st, A);
 }
 
 }  // namespace sift
