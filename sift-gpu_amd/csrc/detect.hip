@@ -292,7 +292,13 @@ __global__ __launch_bounds__(64) void extrema_walk_kernel(WalkArgs A) {
   __shared__ float ring[3][6][kWCols];  // planes: DoG 0..3, Gaussian layers 1, 2
   const int lane = threadIdx.x;
   const int b = blockIdx.y;
-  const int t = blockIdx.x;
+  // XCD-aware order (speed only): blocks b and b + 8 share an XCD, so XCD x
+  // takes the contiguous run [x P, (x + 1) P) of the (octave, chunk, strip)
+  // raster order and neighbouring strips -- which fetch each other's edge
+  // columns -- meet in the same L2
+  const int per_xcd = (int)(gridDim.x >> 3);
+  const int t = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+  if (t >= A.wave_start[A.L.n_oct]) return;
   int o = 0;
   while (o + 1 < A.L.n_oct && A.wave_start[o + 1] <= t) ++o;
   const int local = t - A.wave_start[o];
@@ -730,10 +736,11 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
       w += W.strips[o] * ((L.oct[o].rows + W.chunk - 1) / W.chunk);
     }
     W.wave_start[L.n_oct] = w;
+    const int wg = (w + 7) / 8 * 8;  // whole XCD runs (extra waves exit)
     if (write_dog)
-      hipLaunchKernelGGL(extrema_walk_kernel<true>, dim3(w, batch), dim3(64), 0, st, W);
+      hipLaunchKernelGGL(extrema_walk_kernel<true>, dim3(wg, batch), dim3(64), 0, st, W);
     else
-      hipLaunchKernelGGL(extrema_walk_kernel<false>, dim3(w, batch), dim3(64), 0, st, W);
+      hipLaunchKernelGGL(extrema_walk_kernel<false>, dim3(wg, batch), dim3(64), 0, st, W);
   }
   const MaskLayout& M = A.M;
   hipLaunchKernelGGL(mask_count_kernel, dim3(M.bpw, batch), dim3(256), 0, st, D.mask, M.w_img, M.bpw,
@@ -1099,7 +1106,6 @@ __global__ __launch_bounds__(64) void orient_slots_kernel(RefArgs A) {
   constexpr int NSB = 64 / SB;          // sub-batches per ranked chunk
   constexpr int CH = NSB * SB;          // candidates per ranked chunk (<= 64: one per lane)
   __shared__ float oh[kOSlots][kOGrp][kOriBins + 4];
-  __shared__ float oscr[kOSlots][64];  // scratch words of the lanes not adding at a step
   __shared__ float sm[kOGrp][kOriBins + 4];
   __shared__ int sord[SB];
   __shared__ float etab[64];  // exp32f table, LDS-resident (gathered per sample)
@@ -1236,22 +1242,24 @@ __global__ __launch_bounds__(64) void orient_slots_kernel(RefArgs A) {
       // step jj: lane jj of every group adds its kOSlots samples into the
       // slots' histograms (kOSlots independent rows: reads, one wait, adds,
       // writes); the wave's LDS operations stay in program order, so step
-      // jj + 1 reads what step jj wrote.  Branch-free: the other lanes do the
-      // same read-modify-write on a private scratch word.  (With one guarded
-      // block per step -- mutually exclusive for a single thread -- hipcc
-      // rebuilt the eight blocks as a switch on q and ran the steps out of
-      // order: measured, 3 % of the angles off by a few ulps.)
+      // jj + 1 reads what step jj wrote.  Each step tests a fresh opaque copy
+      // of q behind a compiler barrier: with plain q == jj guards -- eight
+      // mutually exclusive blocks for one thread -- hipcc rebuilt the steps as
+      // a switch on q and ran them out of order (measured: 3 % of the angles
+      // a few ulps off).  (A branch-free form, the other lanes updating a
+      // scratch word, measured 1.54 ms against 1.42: its scratch accesses
+      // share banks with the histogram rows.)
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
-        const bool mine = q == jj;
-        float* p[kOSlots];
+        int qv = q;
+        asm volatile("; orient step %1" : "+v"(qv) : "n"(jj) : "memory");
+        if (qv == jj) {
+          float h[kOSlots];
 #pragma unroll
-        for (int u = 0; u < kOSlots; ++u) p[u] = mine ? &oh[u][g][bin[u]] : &oscr[u][lane];
-        float h[kOSlots];
+          for (int u = 0; u < kOSlots; ++u) h[u] = oh[u][g][bin[u]];
 #pragma unroll
-        for (int u = 0; u < kOSlots; ++u) h[u] = *p[u];
-#pragma unroll
-        for (int u = 0; u < kOSlots; ++u) *p[u] = h[u] + val[u];
+          for (int u = 0; u < kOSlots; ++u) oh[u][g][bin[u]] = h[u] + val[u];
+        }
       }
     }
     wave_sync();
