@@ -4,6 +4,7 @@ for the full SIFT_NCL output (keypoints and descriptors), at small sizes live
 against the oracle and at 1920x1080 against golden SHA-256 digests."""
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -382,3 +383,32 @@ def test_cpp_main_shaped_caller_runs(tmp_path, siftgpu, oracle):
     img = ((i * 7 + j * 13) % 251).astype(np.float32)
     n_ref = len(oracle.sift(img)[0])
     assert f"{n_ref} keypoints, {n_ref} x 128 descriptors" in out, (out, n_ref)
+
+
+_VARIANT_RUN = r"""
+import hashlib, sys
+import numpy as np
+import torch  # noqa: F401  (one process-wide HIP runtime)
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import oracle, siftgpu
+img = oracle.synth_image(0, 1080, 1920)
+with siftgpu.Context(1080, 1920, 1, device=0) as ctx:
+    kps, desc = ctx.SIFT_NCL(img)
+sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+print(len(kps), sha(kps), sha(desc))
+"""
+
+
+@pytest.mark.parametrize("env", [{"SIFT_HIP_EXTREMA_TILES": "1"}, {"SIFT_HIP_ORIENT_SLOTS": "1"},
+                                 {"SIFT_HIP_ORIENT_SLOTS": "3"}, {"SIFT_HIP_ORIENT_SLOTS": "4"},
+                                 {"SIFT_HIP_DESC_PACKED": "0"}])
+def test_kernel_variants_match_golden(env):
+    """The A/B kernel variants the library keeps behind environment switches
+    (read once per process, so each runs in a child process) give the same
+    1080p keypoints and descriptors as the default kernels and the CPU path."""
+    g = load_golden("synth0_1080x1920")
+    r = subprocess.run([sys.executable, "-c", _VARIANT_RUN, PKG, os.path.join(ROOT, "oracle")],
+                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, ksha, dsha = r.stdout.split()[-3:]
+    assert int(n) == int(g["n"]) and ksha == str(g["kp_sha"]) and dsha == str(g["desc_sha"]), env
