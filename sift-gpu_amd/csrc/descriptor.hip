@@ -257,8 +257,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
       float rbin = r_rot + d / 2 - 0.5f;
       float cbin = c_rot + d / 2 - 0.5f;
       const int r = py + i, c = px + j;
-      const bool ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 &&
-                      r < rows - 1 && c > 0 && c < cols - 1;
+      // the row table enumerates interior pixels only (src/sift.cpp:620-621's
+      // 0 < r < rows-1, 0 < c < cols-1), so only the whole-window walk tests them
+      const bool ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d &&
+                      (table || (r > 0 && r < rows - 1 && c > 0 && c < cols - 1));
       const int rcl = min(max(r, 0), rows - 1), ccl = min(max(c, 0), cols - 1);
       const float2 mo_raw = gimg[(long long)rcl * pitch + ccl];  // (Mag, Ori) of the pixel
       // invalid: (0, 0) -- border gradients are never written and may hold NaN
@@ -266,11 +268,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
       const float w = exp32f_v((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
       float obin = (mo.y - ori) * bins_per_rad;
       const float mag = mo.x * w;
-      int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
-      int o0 = cv_floor(obin);
-      rbin -= r0;
-      cbin -= c0;
-      obin -= o0;
+      // cvFloor: |rbin|, |cbin|, |obin| < 10, so floorf is exact and
+      // (int)floorf == cvFloor; rbin - floorf(rbin) == rbin - (float)r0
+      const float fr = floorf(rbin), fc = floorf(cbin), fo = floorf(obin);
+      int r0 = (int)fr, c0 = (int)fc;
+      int o0 = (int)fo;
+      rbin -= fr;
+      cbin -= fc;
+      obin -= fo;
       if (o0 < 0) o0 += nb;
       if (o0 >= nb) o0 -= nb;
       const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
