@@ -106,9 +106,15 @@ __device__ __forceinline__ float exp32f(float v, const float* __restrict__ tab,
 // The same with the table held one entry per lane (lane j: tab[j]) and read
 // with a cross-lane permute instead of an LDS gather; every lane of the wave
 // must execute it.
+// CLAMP = false drops exp32f's input clamp to [lo, hi]: exact for callers whose
+// argument is known to lie inside it (the descriptor's -(c^2 + r^2) / 8 over a
+// window), and still finite outside it (t is clamped below).
+template <bool CLAMP = true>
 __device__ __forceinline__ float exp32f_v(float v, float tab_lane, const ExpConsts& k) {
-  v = v < k.lo ? k.lo : v;
-  v = k.hi < v ? k.hi : v;
+  if (CLAMP) {
+    v = v < k.lo ? k.lo : v;
+    v = k.hi < v ? k.hi : v;
+  }
   v = v * k.prescale;
   int vi = cv_round(v);
   v = (v - (float)vi) * k.post;

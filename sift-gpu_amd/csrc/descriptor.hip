@@ -182,6 +182,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
     const float2* gimg = A.grad + b * A.L.g_img + O.g_off[active ? layer : 0];
     const int rows = O.rows, cols = O.cols;
     const int px = cv_round(ptx), py = cv_round(pty);
+    const int pitch32 = (int)pitch;
+    const int ctr_off = min(max(py, 0), rows - 1) * pitch32 + min(max(px, 0), cols - 1);
     float cos_t = cosf_cr(ori * (float)(kCvPi / 180));
     float sin_t = sinf_cr(ori * (float)(kCvPi / 180));
     const float bins_per_rad = nb / 360.f;
@@ -261,11 +263,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
       // 0 < r < rows-1, 0 < c < cols-1), so only the whole-window walk tests them
       const bool ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d &&
                       (table || (r > 0 && r < rows - 1 && c > 0 && c < cols - 1));
-      const int rcl = min(max(r, 0), rows - 1), ccl = min(max(c, 0), cols - 1);
-      const float2 mo_raw = gimg[(long long)rcl * pitch + ccl];  // (Mag, Ori) of the pixel
+      // an invalid sample gathers from the clamped keypoint centre (any valid
+      // address: its value is replaced below); plane offsets fit 32 bits
+      const float2 mo_raw = gimg[(unsigned)(ok ? r * pitch32 + c : ctr_off)];  // (Mag, Ori) of the pixel
       // invalid: (0, 0) -- border gradients are never written and may hold NaN
       const float2 mo = ok ? mo_raw : make_float2(0.f, 0.f);
-      const float w = exp32f_v((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
+      const float w = exp32f_v<false>((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
       float obin = (mo.y - ori) * bins_per_rad;
       const float mag = mo.x * w;
       // cvFloor: |rbin|, |cbin|, |obin| < 10, so floorf is exact and
