@@ -565,9 +565,9 @@ def main():
         prof = leg([serial], siftgpu.SIFT_FLAG_PROFILE)
     fast = fast_prof = None
     if not a.no_fast and want("fast"):
-        # one stream: with the HBM-heavy separable pyramid the 4-stream split
-        # measured slower (16.05 vs 15.4 ms per step on MI355X)
-        fast = leg([serial], siftgpu.SIFT_FLAG_FAST)
+        # the same --streams split as the exact leg (2 streams: 12.8-12.9 vs
+        # 13.2-13.4 ms per step on one stream, round 2 final tree)
+        fast = leg(parts, siftgpu.SIFT_FLAG_FAST)
         fast_prof = leg([serial], siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
     match = None
     if not (a.no_match or rank != 0 or B < 2 or exact is None):
@@ -682,7 +682,7 @@ def main():
                 "value": round(mpix / fdt, 2), "unit": "Mpix/s", "ms_per_step": round(fdt / a.steps * 1e3, 3),
                 "keypoints_per_s": round(fkp * a.steps / fdt, 1), "keypoints_per_step": int(fkp),
                 "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in fst.items()},
-                "note": "one context, one stream, graph replay; SIFT_FLAG_FAST: separable row/column Gaussian "
+                "note": "the exact leg's stream split (--streams), graph replay; SIFT_FLAG_FAST: separable row/column Gaussian "
                         "pyramid (pyramid_fast.hip) in front of "
                         "the same exact DoG/extrema/orientation/descriptor kernels; not bit-exact (float "
                         "rounding of the pyramid), keypoint/descriptor match rates vs the CPU path are in "
