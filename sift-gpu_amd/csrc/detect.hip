@@ -1101,7 +1101,8 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
 // reference's raster order (src/sift.cpp:429-437); an invalid sample adds +0.0
 // to bin 0 (exact no-op: every bin is >= +0).
 template <int kOSlots>
-__global__ __launch_bounds__(64) void orient_slots_kernel(RefArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2 ? 6 : 1))) void orient_slots_kernel(
+    RefArgs A) {
   constexpr int SB = kOGrp * kOSlots;   // candidates per sub-batch
   constexpr int NSB = 64 / SB;          // sub-batches per ranked chunk
   constexpr int CH = NSB * SB;          // candidates per ranked chunk (<= 64: one per lane)
