@@ -78,12 +78,13 @@ __device__ __forceinline__ void slab(float a, float b, int& lo, int& hi) {
 // Record hand-off, two forms (same sums, same bits):
 //   PACKED = false: records (qidx, value) as float2 at [sample][group][owner]
 //     (4.2 KB), a 32-bit row table (2.6 KB): 12.4 KB of LDS per wave;
-//   PACKED = true: values at [group][owner][sample] (2.1 KB, the owner reads
-//     its 8 values with two ds_read_b128), bin bytes at [group][owner][sample]
-//     (0.5 KB, one ds_read_b64), a 16-bit row table (1.3 KB): 9.4 KB per
-//     wave, and the in-flight records packed as 8 values + 2 words of bin
-//     bytes, so four waves per SIMD fit instead of three.
-constexpr int kRecG = 68;  // PACKED value words per group (8 owners x 8 samples + pad: b128 reads conflict free)
+//   PACKED = true: values at [group][owner][sample] (2 KB, XOR-swizzled so
+//     the owner's two ds_read_b128 are conflict free and each store address
+//     is one XOR), bin bytes at [group][owner][sample] (0.5 KB, one
+//     ds_read_b64), a 16-bit row table (1.3 KB): 9.4 KB per wave, and the
+//     in-flight records packed as 8 values + 2 words of bin bytes, so four
+//     waves per SIMD fit instead of three.
+constexpr int kRecG = 64;  // PACKED value words per group (8 owners x 8 samples, XOR-swizzled, see the store)
 
 template <bool PACKED>
 struct RecT {  // one lane's 8 corner records: (qidx, value) pairs
@@ -352,14 +353,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
     }
     for (int base = 0; base < nmax; base += 8) {
       if constexpr (PACKED) {
-        // corner k to owner slot s = k ^ odd: value at [g][s][q], bin byte at [g][s][q]
-        float* dv = rec + g * kRecG + q;
-        unsigned char* dq = recq + g * 64 + q;
+        // corner k to owner slot s = k ^ odd: value at byte (g << 8) | (s << 5) |
+        // (q << 2), bit 4 flipped on odd groups (so a 16-lane pass of the
+        // owners' ds_read_b128 -- an even and an odd group -- covers all 64
+        // banks); bin byte at (g << 6) | (s << 3) | q.  Slot bits are clear
+        // in both bases, so each address is one XOR with k's slot bits.
+        char* rb = reinterpret_cast<char*>(rec);
+        const int wv = ((g << 8) | ((q << 2) ^ ((g & 1) << 4))) | (odd_cur << 5);
+        const int wq = ((g << 6) | q) | (odd_cur << 3);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int sl = (k ^ odd_cur) * 8;
-          dv[sl] = rc_cur.v[k];
-          dq[sl] = (unsigned char)(rc_cur.qb[k >> 2] >> (8 * (k & 3)));
+          *reinterpret_cast<float*>(rb + (wv ^ (k << 5))) = rc_cur.v[k];
+          recq[wq ^ (k << 3)] = (unsigned char)(rc_cur.qb[k >> 2] >> (8 * (k & 3)));
         }
       } else {
         float2* dst2 = reinterpret_cast<float2*>(rec + q * kRecStride2 + g * 16);
@@ -375,8 +380,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
       sample(base + 8 + q < nsamp, rc_nxt, odd_nxt);
       // ordered accumulation of batch k: lane q applies its record of each sample
       if constexpr (PACKED) {
-        const float4* sv = reinterpret_cast<const float4*>(rec + g * kRecG + q * 8);
-        const float4 va = sv[0], vb = sv[1];
+        const char* rb = reinterpret_cast<const char*>(rec);
+        const int rv = (g << 8) | (q << 5);  // samples 0-3 at bit 4 = g & 1, samples 4-7 at the other half
+        const float4 va = *reinterpret_cast<const float4*>(rb + (rv | ((g & 1) << 4)));
+        const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | (((g & 1) ^ 1) << 4)));
         const uint2 qq = *reinterpret_cast<const uint2*>(recq + lane * 8);
         const float vals[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
