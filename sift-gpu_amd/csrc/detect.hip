@@ -792,13 +792,54 @@ __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const flo
   Refined R{};
   R.ok = true;
   int it = 0;
-  auto D = [&](int l, int yy, int xx) -> float {
-    const long long p = (long long)yy * pitch + xx;
-    if (FROM_G) return gimg[O.g_off[l + 1] + p] - gimg[O.g_off[l] + p];
-    return dimg[O.d_off[l] + p];
+  // The 3x3 neighbourhood of (r, c) in DoG layers layer-1 .. layer+1, loaded
+  // once per Newton step as one 12-byte row per plane and row (FROM_G: four
+  // Gaussian planes, DoG = g[l+1] - g[l], src/sift.cpp:276 -- the same float
+  // subtraction as the stored DoG, bit-identical).  (r, c) stays >= 5 from
+  // the border and layer in [1, 2], so every row lies inside its plane.
+  struct Row3 {
+    float a, b, c;
   };
-#define AT(pl, yy, xx) D(pl, yy, xx)
+  float cube[3][3][3];  // [layer - (cur - 1)][dy + 1][dx + 1]
+  int cube_layer = -1, cube_r = -1, cube_c = -1;
+  auto load_cube = [&](int cur, int rr_, int cc_) {
+    if (cur == cube_layer && rr_ == cube_r && cc_ == cube_c) return;
+    cube_layer = cur;
+    cube_r = rr_;
+    cube_c = cc_;
+    const long long base = (long long)(rr_ - 1) * pitch + (cc_ - 1);
+    if (FROM_G) {
+      Row3 gv[4][3];
+#pragma unroll
+      for (int pl = 0; pl < 4; ++pl)
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+          gv[pl][dy] = *reinterpret_cast<const Row3*>(gimg + O.g_off[cur - 1 + pl] + base + dy * pitch);
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          cube[l][dy][0] = gv[l + 1][dy].a - gv[l][dy].a;
+          cube[l][dy][1] = gv[l + 1][dy].b - gv[l][dy].b;
+          cube[l][dy][2] = gv[l + 1][dy].c - gv[l][dy].c;
+        }
+    } else {
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const Row3 v = *reinterpret_cast<const Row3*>(dimg + O.d_off[cur - 1 + l] + base + dy * pitch);
+          cube[l][dy][0] = v.a;
+          cube[l][dy][1] = v.b;
+          cube[l][dy][2] = v.c;
+        }
+    }
+  };
+// DoG value of layer pl at (yy, xx): every use is within one of (layer, r, c),
+// so the cube indices fold to constants
+#define AT(pl, yy, xx) cube[(pl) - (layer - 1)][(yy) - r + 1][(xx) - c + 1]
   for (; it < kMaxInterp; ++it) {
+    load_cube(layer, r, c);
     const int cur = layer, lo = layer - 1, hi = layer + 1;
     const float g[3] = {(AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale,
                         (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale,
@@ -839,6 +880,7 @@ __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const flo
     return R;
   }
   {
+    load_cube(layer, r, c);  // unchanged since the last step's load (the loop left without moving)
     const int cur = layer, lo = layer - 1, hi = layer + 1;
     const float g0 = (AT(cur, r, c + 1) - AT(cur, r, c - 1)) * deriv_scale;
     const float g1 = (AT(cur, r + 1, c) - AT(cur, r - 1, c)) * deriv_scale;
