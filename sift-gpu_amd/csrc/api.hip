@@ -380,10 +380,10 @@ void enqueue_detect(sift_ctx* c, const Layout& L, int batch, sift_keypoint* kpts
 }
 
 void enqueue_desc(sift_ctx* c, const Layout& L, const sift_keypoint* kpts, const int* img_off,
-                  int batch, int kp_cap, float* desc, int first_octave) {
+                  int batch, int kp_cap, float* desc, int first_octave, bool detected) {
   StageScope s(c, ST_DESC);
   launch_descriptors(c->stream, L, c->d_grad, c->d_mc, kpts, img_off, batch, kp_cap, desc,
-                     first_octave, c->d_err);
+                     first_octave, c->d_err, detected);
 }
 
 // End of every compute sequence: status_kernel folds the candidate and
@@ -769,7 +769,7 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
     (void)hipEventRecord(v1, c->stream);
     enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
     (void)hipEventRecord(v2, c->stream);
-    enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
+    enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0, true);
     (void)hipEventRecord(v3, c->stream);
     enqueue_status(c, true, d_img_offsets, batch, kp_cap);
     verbose_phase(c, "pyramid construction time", v0, v1);
@@ -796,7 +796,7 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
   return run_graphed(c, key, [&]() {
     enqueue_pyramid(c, L, src, batch, false);
     enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
-    enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0);
+    enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0, true);
     enqueue_status(c, true, d_img_offsets, batch, kp_cap);
   });
 }
@@ -1012,7 +1012,7 @@ int sift_calc_descriptors(sift_ctx* c, const float* gpyr, int rows, int cols, in
                             c->stream));
   // keypoints may name any scale 0..4 (CV_Assert at src/sift.cpp:744): gradients of all five
   launch_grad(c->stream, L, c->d_gpyr, c->d_grad, 1, 0, kScales - 1, c->d_mc);
-  enqueue_desc(c, L, c->d_kpts, c->d_img_off, 1, c->kp_cap, c->d_desc, first_octave);
+  enqueue_desc(c, L, c->d_kpts, c->d_img_off, 1, c->kp_cap, c->d_desc, first_octave, false);
   enqueue_status(c, false, nullptr, 1, c->kp_cap);  // no detection ran: assertion bit only
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -96,7 +96,10 @@ struct RecT<true> {
   unsigned qb[2];  // qidx of corner k in byte k & 3 of word k >> 2
 };
 
-template <bool PACKED>
+// DET: the keypoints come from this library's detection, so every window has
+// radius <= 40 (scl < 1.6 * 2^1.25, src/sift.cpp:588) and a row table: the
+// whole-window walk and its interior tests compile away.
+template <bool PACKED, bool DET>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 : 1))) void descriptor_kernel(
     DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
@@ -193,10 +196,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
     int radius = cv_round(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
     const int diag = (int)sqrt(((double)cols) * cols + ((double)rows) * rows);
     radius = radius < diag ? radius : diag;
+    if (DET) radius = min(radius, (kMaxWinRows - 1) / 2);  // a no-op for detected keypoints (<= 40); keeps the table in bounds
     cos_t /= hist_width;
     sin_t /= hist_width;
     const int D = active ? 2 * radius + 1 : 0;
-    const bool table = D <= kMaxWinRows;
+    const bool table = DET || D <= kMaxWinRows;
     // ---- per-row candidate j-ranges and the sample count ----
     int nsamp = 0;
     if (table) {
@@ -498,7 +502,7 @@ void launch_math_selftest(hipStream_t st, int op, const float* a, const float* b
 
 void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, const MathConsts* mc,
                         const sift_keypoint* kpts, const int* img_kp_off, int batch, int kp_cap,
-                        float* desc, int first_octave, int* err_flag) {
+                        float* desc, int first_octave, int* err_flag, bool detected) {
   DescArgs A;
   A.L = L;
   A.grad = grad;
@@ -514,12 +518,17 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
     const char* e = getenv("SIFT_HIP_DESC_PACKED");  // A/B switch between the two record forms
     return !e || atoi(e) != 0;
   }();
-  if (packed)
-    hipLaunchKernelGGL(descriptor_kernel<true>, dim3(resident_grid((const void*)descriptor_kernel<true>, 64, 0, 8192)),
-                       dim3(64), 0, st, A);
+  if (packed && detected)
+    hipLaunchKernelGGL((descriptor_kernel<true, true>),
+                       dim3(resident_grid((const void*)descriptor_kernel<true, true>, 64, 0, 8192)), dim3(64), 0, st, A);
+  else if (packed)
+    hipLaunchKernelGGL((descriptor_kernel<true, false>),
+                       dim3(resident_grid((const void*)descriptor_kernel<true, false>, 64, 0, 8192)), dim3(64), 0, st,
+                       A);
   else
-    hipLaunchKernelGGL(descriptor_kernel<false>,
-                       dim3(resident_grid((const void*)descriptor_kernel<false>, 64, 0, 8192)), dim3(64), 0, st, A);
+    hipLaunchKernelGGL((descriptor_kernel<false, false>),
+                       dim3(resident_grid((const void*)descriptor_kernel<false, false>, 64, 0, 8192)), dim3(64), 0,
+                       st, A);
 }
 
 }  // namespace sift
