@@ -59,13 +59,16 @@ struct DescArgs {
 };
 
 // Narrow [lo, hi] to the j with |j*a + b| < 2.5 (+ margin).
-__device__ __forceinline__ void slab(float a, float b, int& lo, int& hi) {
+// inv_a = 1 / a (per keypoint): the bounds only have to enclose the samples
+// the exact predicate keeps, and the margin (>= 0.057 in j for |a| <= 1/5.7)
+// dwarfs the rounding of a multiply by the reciprocal.
+__device__ __forceinline__ void slab(float a, float inv_a, float b, int& lo, int& hi) {
   const float lim = 2.5f + 1e-2f;  // margin >> float rounding of r_rot / c_rot
   if (fabsf(a) < 1e-12f) {
     if (!(fabsf(b) < lim)) hi = lo - 1;
     return;
   }
-  float x0 = (-lim - b) / a, x1 = (lim - b) / a;
+  float x0 = (-lim - b) * inv_a, x1 = (lim - b) * inv_a;
   if (x0 > x1) {
     const float t = x0;
     x0 = x1;
@@ -199,6 +202,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
     if (DET) radius = min(radius, (kMaxWinRows - 1) / 2);  // a no-op for detected keypoints (<= 40); keeps the table in bounds
     cos_t /= hist_width;
     sin_t /= hist_width;
+    const float inv_sin = fabsf(sin_t) < 1e-12f ? 0.f : 1.f / sin_t;
+    const float inv_cos = fabsf(cos_t) < 1e-12f ? 0.f : 1.f / cos_t;
     const int D = active ? 2 * radius + 1 : 0;
     const bool table = DET || D <= kMaxWinRows;
     // ---- per-row candidate j-ranges and the sample count ----
@@ -208,8 +213,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
         const int i = ri - radius;
         int lo = max(-radius, 1 - px), hi = min(radius, cols - 2 - px);  // 0 < px + j < cols-1
         if (!(py + i > 0 && py + i < rows - 1)) hi = lo - 1;
-        slab(sin_t, i * cos_t, lo, hi);     // r_rot = j*sin_t + i*cos_t
-        slab(cos_t, -(i * sin_t), lo, hi);  // c_rot = j*cos_t - i*sin_t
+        slab(sin_t, inv_sin, i * cos_t, lo, hi);     // r_rot = j*sin_t + i*cos_t
+        slab(cos_t, inv_cos, -(i * sin_t), lo, hi);  // c_rot = j*cos_t - i*sin_t
         const int len = hi >= lo ? hi - lo + 1 : 0;
         rows_tab[g][ri] = len ? (lo + 64) | (len << kLenSh) : 0;  // lo in [-40, 40] when len > 0
         nsamp += len;
