@@ -89,10 +89,13 @@ struct ExpConsts {
   float A1, A2, A3, A4, lo, hi, post, prescale;
 };
 
+template <bool CLAMP = true>  // false: see exp32f_v
 __device__ __forceinline__ float exp32f(float v, const float* __restrict__ tab,
                                         const ExpConsts& k) {
-  v = v < k.lo ? k.lo : v;
-  v = k.hi < v ? k.hi : v;
+  if (CLAMP) {
+    v = v < k.lo ? k.lo : v;
+    v = k.hi < v ? k.hi : v;
+  }
   v = v * k.prescale;
   int vi = cv_round(v);
   v = (v - (float)vi) * k.post;
