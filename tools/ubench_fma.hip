@@ -9,11 +9,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 // OP: 0 v_fma_f32, 1 v_pk_fma_f32, 2 v_add_f32, 3 v_pk_add_f32.  Every case
 // does 16 lane-ops per inner step (16 scalar or 8 packed instructions).
-template <int OP>
-__global__ __launch_bounds__(256) void op_kernel(float* out, int iters, float k) {
+// VG: the addend / multiplier in a VGPR (k + s * 0, not foldable under IEEE
+// rules) instead of the kernel-argument SGPR.
+template <int OP, bool VG>
+__global__ __launch_bounds__(256) void op_kernel(float* out, int iters, float k0) {
   extern __shared__ float pad[];
   if (iters < 0) pad[threadIdx.x] = 0.f;  // keeps the LDS allocation (occupancy control)
   const float s = threadIdx.x * 1e-3f;
+  const float k = VG ? k0 + s * 0.f : k0;
   float r = 0.f;
   if (OP == 1 || OP == 3) {
     f2 a[8];
@@ -44,7 +47,7 @@ __global__ __launch_bounds__(256) void op_kernel(float* out, int iters, float k)
   out[blockIdx.x * 256 + threadIdx.x] = r;
 }
 
-template <int OP>
+template <int OP, bool VG>
 void run(const char* name, int ncu, float* out) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -55,7 +58,7 @@ void run(const char* name, int ncu, float* out) {
     const int grid = ncu * wps;
     for (int rep = 0; rep < 2; ++rep) {
       hipEventRecord(e0);
-      hipLaunchKernelGGL(op_kernel<OP>, dim3(grid), dim3(256), lds, 0, out, iters, 0.999f);
+      hipLaunchKernelGGL((op_kernel<OP, VG>), dim3(grid), dim3(256), lds, 0, out, iters, 0.999f);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms = 0;
@@ -63,9 +66,9 @@ void run(const char* name, int ncu, float* out) {
       const double lane_ops = (double)grid * 256 * iters * 8 * 16;
       const double instr_per_simd = lane_ops / 64 / (OP == 1 || OP == 3 ? 2 : 1) / (ncu * 4);
       if (rep)
-        printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"Tlane_ops\": %.1f, "
+        printf("{\"op\": \"%s\", \"operand\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"Tlane_ops\": %.1f, "
                "\"ns_per_instr_per_simd\": %.3f}\n",
-               name, wps, ms, lane_ops / ms / 1e9, ms * 1e6 / instr_per_simd);
+               name, VG ? "vgpr" : "sgpr", wps, ms, lane_ops / ms / 1e9, ms * 1e6 / instr_per_simd);
     }
   }
   hipEventDestroy(e0);
@@ -77,10 +80,12 @@ int main() {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) return 1;
   float* out = nullptr;
   if (hipMalloc(&out, 256 * 8 * 4096 * sizeof(float)) != hipSuccess) return 1;
-  run<0>("v_fma_f32", ncu, out);
-  run<1>("v_pk_fma_f32", ncu, out);
-  run<2>("v_add_f32", ncu, out);
-  run<3>("v_pk_add_f32", ncu, out);
+  run<0, false>("v_fma_f32", ncu, out);
+  run<1, false>("v_pk_fma_f32", ncu, out);
+  run<2, false>("v_add_f32", ncu, out);
+  run<3, false>("v_pk_add_f32", ncu, out);
+  run<2, true>("v_add_f32", ncu, out);
+  run<3, true>("v_pk_add_f32", ncu, out);
   (void)hipFree(out);
   return 0;
 }
