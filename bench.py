@@ -147,7 +147,13 @@ def cpu_baseline_parallel(rows, cols, workers):
                               env=dict(os.environ, OMP_NUM_THREADS="1", HIP_VISIBLE_DEVICES="",
                                        CUDA_VISIBLE_DEVICES=""))
              for i in range(workers)]
-    outs = [p.communicate(timeout=600)[0].split() for p in procs]
+    try:
+        outs = [p.communicate(timeout=600)[0].split() for p in procs]
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            p.kill()
+            p.wait()
+        raise
     wall = time.perf_counter() - t0
     if any(p.returncode for p in procs):
         return None
@@ -432,93 +438,109 @@ def match_cpu_baseline(m, n_sample=64):
             "gpu_equals_oracle_on_sample": same}
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    cpu = None
-    if world == 1 and not a.no_cpu_baseline and a.only is None:
-        # before this process touches the GPU: the image-parallel leg starts
-        # child processes
-        nthr = min(16, int(os.environ.get("OMP_NUM_THREADS", "16")))
-        cpu = {"cpu_baseline": cpu_baseline(a.rows, a.cols),
-               "cpu_baseline_omp": cpu_baseline(a.rows, a.cols, nthr)}
-        par = cpu_baseline_parallel(a.rows, a.cols, nthr)
-        if par:
-            cpu["cpu_baseline_all_cores"] = par
-        cpu["cpu_host"] = {"nproc": os.cpu_count(), "model": _cpu_model(), "share_used": nthr,
-                           "compiler_flags": "gcc -O3 -ffp-contract=off -fno-fast-math"}
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
-    B, R, C = a.batch, a.rows, a.cols
-    S = max(1, min(a.streams, B // 2))
-    seed_base = rank * B
-    imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
-    gathering = world > 1 and not a.no_gather
-    gathered = {"steps": 0, "keypoints": 0}
+def guarded(errors, name, fn, *args, **kw):
+    """Runs one optional leg; a failure is recorded as errors[name] and the
+    leg's block as {"error": ...} instead of costing the headline line."""
+    try:
+        return fn(*args, **kw)
+    except Exception as e:  # noqa: BLE001 -- any failure of an optional leg
+        errors[name] = f"{type(e).__name__}: {e}"[:400]
+        print(f"bench.py: leg {name} failed: {errors[name]}", file=sys.stderr, flush=True)
+        return None
 
-    class Part:
-        """One context on one stream over images [b0, b0 + nb) of this rank's
-        batch; with `gather`, its results go to rank 0 one step behind
-        (sift_dist.PipelinedSteps, two result slots)."""
 
-        def __init__(self, b0, nb, strm, gather):
-            self.b0, self.nb, self.stream = b0, nb, strm
-            self.ctx = siftgpu.Context(R, C, nb, device=dev)
-            self.ctx.set_stream(strm.cuda_stream)
-            self.ctx.set_octaves(a.octaves)
-            self.cap = nb * 40000
-            self.bufs = [(torch.empty((self.cap, 7), dtype=torch.int32, device="cuda"),
-                          torch.empty((self.cap, 128), dtype=torch.float32, device="cuda"),
-                          torch.empty((nb + 1,), dtype=torch.int32, device="cuda")) for _ in range(2 if gather else 1)]
-            self.runner = None
-            if gather:
-                def on_result(step, out, first=(b0 == 0)):
-                    gathered["steps"] += 1 if first else 0
-                    gathered["keypoints"] += sum(int(o[-1]) for o in out[1])
-                pipe = sift_dist.GatherPipeline([nb] * world, self.cap, dst=0)
-                self.runner = sift_dist.PipelinedSteps(pipe, self.bufs, with_desc=False, on_result=on_result)
+def cpu_legs(a, errors):
+    """1 thread, OpenMP over descriptors, image-parallel."""
+    nthr = min(16, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    cpu = {}
+    one = guarded(errors, "cpu_baseline", cpu_baseline, a.rows, a.cols)
+    if one is not None:
+        cpu["cpu_baseline"] = one
+    omp = guarded(errors, "cpu_baseline_omp", cpu_baseline, a.rows, a.cols, nthr)
+    if omp is not None:
+        cpu["cpu_baseline_omp"] = omp
+    par = guarded(errors, "cpu_baseline_all_cores", cpu_baseline_parallel, a.rows, a.cols, nthr)
+    if par:
+        cpu["cpu_baseline_all_cores"] = par
+    cpu["cpu_host"] = {"nproc": os.cpu_count(), "model": _cpu_model(), "share_used": nthr,
+                       "compiler_flags": "gcc -O3 -ffp-contract=off -fno-fast-math"}
+    return cpu
 
-        def compute(self, k, d, o):
-            self.ctx.detect_compute_batch(imgs[self.b0].data_ptr(), self.nb, R, C, C, R * C, k.data_ptr(),
-                                          d.data_ptr(), self.cap, o.data_ptr())
 
-        def step(self):
-            with torch.cuda.stream(self.stream):
-                if self.runner is not None:
-                    self.runner.step(self.compute)
-                else:
-                    self.compute(*self.bufs[0])
+class Part:
+    """One context on one stream over images [b0, b0 + nb) of this rank's
+    batch; with `gather`, its results go to rank 0 one step behind
+    (sift_dist.PipelinedSteps, two result slots)."""
 
-        def flush(self):
+    def __init__(self, env, b0, nb, strm, gather):
+        self.env, self.b0, self.nb, self.stream = env, b0, nb, strm
+        R, C = env.R, env.C
+        self.ctx = siftgpu.Context(R, C, nb, device=env.dev)
+        self.ctx.set_stream(strm.cuda_stream)
+        self.ctx.set_octaves(env.octaves)
+        self.cap = nb * 40000
+        self.bufs = [(torch.empty((self.cap, 7), dtype=torch.int32, device="cuda"),
+                      torch.empty((self.cap, 128), dtype=torch.float32, device="cuda"),
+                      torch.empty((nb + 1,), dtype=torch.int32, device="cuda")) for _ in range(2 if gather else 1)]
+        self.runner = self.pipe = None
+        if gather:
+            def on_result(step, out, first=(b0 == 0)):
+                env.gathered["steps"] += 1 if first else 0
+                env.gathered["keypoints"] += sum(int(o[-1]) for o in out[1])
+            self.pipe = sift_dist.GatherPipeline(env.shard_batches(nb), self.cap, dst=0)
+            self.runner = sift_dist.PipelinedSteps(self.pipe, self.bufs, with_desc=False, on_result=on_result)
+
+    def compute(self, k, d, o):
+        e = self.env
+        self.ctx.detect_compute_batch(e.imgs[self.b0].data_ptr(), self.nb, e.R, e.C, e.C, e.R * e.C, k.data_ptr(),
+                                      d.data_ptr(), self.cap, o.data_ptr())
+
+    def step(self):
+        with torch.cuda.stream(self.stream):
             if self.runner is not None:
-                with torch.cuda.stream(self.stream):
-                    self.runner.flush()
+                self.runner.step(self.compute)
+            else:
+                self.compute(*self.bufs[0])
 
-        def close(self):
-            self.ctx.close()
+    def flush(self):
+        if self.runner is not None:
+            with torch.cuda.stream(self.stream):
+                self.runner.flush()
 
-    # The timed step: the batch as S sub-batches, one context and HIP stream
-    # each, no synchronisation between them inside the timed region -- the
-    # streams drift out of phase, so one's descriptor phase runs beside
-    # another's blur (DESIGN.md 6-7).  Per-kernel rooflines and stage times
-    # come from a separate serial leg: one context, the whole batch, HIP events
-    # around every stage (concurrent kernels would inflate each other's times).
-    parts = [Part(B * s // S, B * (s + 1) // S - B * s // S,
-                  torch.cuda.Stream() if S > 1 else torch.cuda.current_stream(), gathering) for s in range(S)]
-    serial = Part(0, B, torch.cuda.current_stream(), False)
-    serial.ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=seed_base)
-    torch.cuda.synchronize()
+    def close(self):
+        self.ctx.close()
 
-    def leg(ps, flags):
+
+class Env:
+    """This rank's device state: the synthetic batch, the timed parts and the
+    serial (profiled) part."""
+
+    def __init__(self, a, world, rank):
+        self.a, self.world, self.rank = a, world, rank
+        self.dev = torch.cuda.current_device()
+        self.B, self.R, self.C, self.octaves = a.batch, a.rows, a.cols, a.octaves
+        self.S = max(1, min(a.streams, self.B // 2))
+        self.seed_base = rank * self.B
+        self.imgs = torch.empty((self.B, self.R, self.C), dtype=torch.float32, device="cuda")
+        self.gathering = world > 1 and not a.no_gather
+        self.gathered = {"steps": 0, "keypoints": 0}
+        B, S = self.B, self.S
+        self.parts = [Part(self, B * s // S, B * (s + 1) // S - B * s // S,
+                           torch.cuda.Stream() if S > 1 else torch.cuda.current_stream(), self.gathering)
+                      for s in range(S)]
+        self.serial = Part(self, 0, B, torch.cuda.current_stream(), False)
+        self.serial.ctx.synth_images(self.imgs.data_ptr(), B, self.R, self.C, self.C, self.R * self.C,
+                                     seed_base=self.seed_base)
+        torch.cuda.synchronize()
+
+    def shard_batches(self, nb):
+        return [nb] * self.world   # every rank runs the same --batch / --streams split
+
+    def leg(self, ps, flags):
         """W warmup + K timed steps of parts ps in one mode; returns (max-over-
         ranks seconds, per-stage device stats of this rank (one part), keypoints
         per step summed over ranks)."""
+        a, world = self.a, self.world
         for p in ps:
             p.ctx.set_flags(flags)
         for _ in range(a.warmup):
@@ -529,6 +551,8 @@ def main():
         for p in ps:
             p.ctx.sync()  # sticky device status: candidate / keypoint capacity
             p.ctx.stage_stats(reset=True)
+            if p.pipe is not None:
+                p.pipe.reset_stats()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -554,184 +578,288 @@ def main():
             dist.all_reduce(kp_step, op=dist.ReduceOp.SUM)
         return float(t.item()), stats, float(kp_step.item())
 
-    want = (lambda leg_name: a.only in (None, leg_name))
-    exact = prof = None
-    verified, failed = ([], [])
-    if want("exact"):
-        exact = leg(parts, 0)
-        if rank == 0:
-            verified, failed = verify_outputs([(p.b0, p.nb) + p.bufs[0] for p in parts], R, C, a.octaves,
-                                              seed_base)
-        prof = leg([serial], siftgpu.SIFT_FLAG_PROFILE)
-    fast = fast_prof = None
-    if not a.no_fast and want("fast"):
-        # the same --streams split as the exact leg (2 streams: 12.8-12.9 vs
-        # 13.2-13.4 ms per step on one stream, round 2 final tree)
-        fast = leg(parts, siftgpu.SIFT_FLAG_FAST)
-        fast_prof = leg([serial], siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
-    match = None
-    if not (a.no_match or rank != 0 or B < 2 or exact is None):
-        serial.ctx.set_flags(0)
-        serial.compute(*serial.bufs[0])
-        serial.ctx.sync()
-        match = match_leg(serial.ctx, a, serial.bufs[0][1], serial.bufs[0][2])
-    single = None
-    if rank == 0 and world == 1 and not a.no_single and want("single"):
-        single = single_image_leg(R, C, a.steps, a.warmup)
-    eightk = None
-    if rank == 0 and world == 1 and not a.no_8k and want("8k"):
-        eightk = eightk_leg(a.steps, a.warmup)
+    def gather_evidence(self, dt):
+        """N > 1: per-rank gather statistics of the timed exact leg, collected
+        on rank 0 (gloo metadata group): backend, world size, records each rank
+        sent / rank 0 received, and the side-stream transfer time as a share of
+        the timed region."""
+        mine = {"sent_records": 0, "received_records_per_rank": [0] * self.world, "transfer_ms": 0.0,
+                "gathers": 0}
+        for p in self.parts:
+            if p.pipe is None:
+                continue
+            st = p.pipe.stats()
+            mine["sent_records"] += st["sent_records"]
+            mine["gathers"] += st["gathers"]
+            mine["received_records_per_rank"] = [x + y for x, y in zip(mine["received_records_per_rank"],
+                                                                      st["received_records_per_rank"])]
+            mine["transfer_ms"] += st["transfer_ms"] or 0.0
+        allst = [None] * self.world
+        dist.all_gather_object(allst, mine, group=sift_dist._meta_group())
+        if self.rank != 0:
+            return None
+        recv = allst[0]["received_records_per_rank"]
+        sent = [s["sent_records"] for s in allst]
+        return {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                "steps_gathered": self.gathered["steps"],
+                "keypoints_gathered_per_step": self.gathered["keypoints"] / max(self.gathered["steps"], 1),
+                "received_records_per_rank": recv, "sent_records_per_rank": sent,
+                "sent_equals_received": all(recv[r] == sent[r] for r in range(1, self.world)),
+                "transfer_ms_per_rank": [round(s["transfer_ms"], 3) for s in allst],
+                "transfer_share_of_timed_region": [round(s["transfer_ms"] / (dt * 1e3), 4) for s in allst],
+                "note": "keypoint records (28 B) of every rank's sub-batches gathered to rank 0 one step "
+                        "behind compute (batch_isend_irecv on a side stream); transfer_ms = device time of "
+                        "those transfer groups summed over the timed leg, overlapped with compute"}
 
+    def close(self):
+        for p in self.parts + [self.serial]:
+            p.close()
+
+
+def run_exact(env):
+    """The headline: the exact leg (timed streams) + its output check + the
+    serial profiled leg (stage times, rooflines)."""
+    exact = env.leg(env.parts, 0)
+    verified, failed = [], []
+    if env.rank == 0:
+        verified, failed = verify_outputs([(p.b0, p.nb) + p.bufs[0] for p in env.parts], env.R, env.C,
+                                          env.octaves, env.seed_base)
+    gather = env.gather_evidence(exact[0]) if env.gathering else None
+    prof = env.leg([env.serial], siftgpu.SIFT_FLAG_PROFILE)
+    return {"exact": exact, "prof": prof, "verified": verified, "failed": failed, "gather": gather}
+
+
+def run_fast(env):
+    # the same --streams split as the exact leg (2 streams: 12.8-12.9 vs
+    # 13.2-13.4 ms per step on one stream, round 2 final tree)
+    fast = env.leg(env.parts, siftgpu.SIFT_FLAG_FAST)
+    fast_prof = env.leg([env.serial], siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
+    return fast, fast_prof
+
+
+def run_match(env):
+    s = env.serial
+    s.ctx.set_flags(0)
+    s.compute(*s.bufs[0])
+    s.ctx.sync()
+    return match_leg(s.ctx, env.a, s.bufs[0][1], s.bufs[0][2])
+
+
+def exact_block(a, world, B, R, C, S, res, tr):
+    """The headline fields from run_exact's result."""
+    out = {}
+    dt, _, kp_total_step = res["exact"]
+    pdt, stats, _ = res["prof"]   # stage times / rooflines: the serial profiled leg
+    verified, failed = res["verified"], res["failed"]
+    mpix = world * B * R * C * a.steps / 1e6
+    value = mpix / dt
+
+    # roofline of the dominant kernel: the exact octave blur -- octave 0
+    # in scatter form (blur_sym_kernel) when the library chose it for
+    # this launch size, the 2-D tiles (blur_octave_kernel) otherwise
+    def blur_roof(stage, kernel):
+        bo = stats.get(stage)
+        if not bo or not bo["launches"]:
+            return None
+        per_launch_ms = bo["ms"] / bo["launches"]
+        tflops = (bo["flops"] / bo["launches"]) / (per_launch_ms * 1e-3) / 1e12 if per_launch_ms else 0.0
+        traffic, tsrc = traffic_of(tr, kernel)
+        r = {"bound": "valu", "achieved": round(tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+             "traffic_algorithmic": round(bo["bytes"] / bo["launches"]),
+             "traffic_source": tsrc, "kernel": kernel, "launches_per_step": bo["launches"] // a.steps,
+             "avg_launch_ms": round(per_launch_ms, 4),
+             "valu_issue_frac": valu_issue_frac(tr, kernel, per_launch_ms),
+             "note": "exact-mode 2-D blur is fp32-VALU bound, no MFMA; peak = the fp32 vector peak "
+                     "(FMA counted as 2 flops); flops = 2 x taps per launch, algorithmic (the "
+                     "reference's chain: one multiply + one add per tap, FMA forbidden by the parity "
+                     "contract), 4 scales x the whole batch; traffic = HBM bytes per launch from the "
+                     "committed rocprofv3 PMC pass (calibrated FETCH_SIZE/WRITE_SIZE); valu_issue_frac = "
+                     "SQ_INSTS_VALU per launch (same PMC pass) / launch time / the wave64 VALU issue peak "
+                     "(256 CU x 4 SIMD x 2.4 GHz / 2 cycles)"}
+        if kernel == "blur_sym_kernel":
+            r["note"] += ("; scatter form: K[a][b] = K[-a][b], so each multiply serves kernel rows +a "
+                          "and -a of two outputs -- (2w+1)(w+1) multiplies + (2w+1)^2 adds per output "
+                          "instead of 2(2w+1)^2, same chain, bit-exact -- which is why frac can pass 0.5")
+        return r
+    sym_used = "blur_octave_sym" in stats
+    roof = blur_roof("blur_octave_sym", "blur_sym_kernel") if sym_used else \
+        blur_roof("blur_octave", "blur_octave_kernel")
+    roof_gather = blur_roof("blur_octave", "blur_octave_kernel") if sym_used else None
+    pyr_ms = sum(stats[k]["ms"] for k in ("blur_base", "blur_octave", "blur_octave_sym", "decimate", "dog")
+                 if k in stats)
+    pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
+    gathering = res.get("gather") is not None
+    out.update({
+        "value": round(value, 2),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: integer-exact 1920x1080 textures (SURVEY.md 8(d) d2) generated on device",
+        "config": {"workload": f"configs[2]: batch of {B} x {C}x{R} synthetic grayscale per GPU "
+                               f"(N=8 x 64 = configs[3]), {a.octaves} octaves x 5 scales, exact mode",
+                   "global_batch": world * B, "rows": R, "cols": C, "octaves": a.octaves,
+                   "mode": "exact (bit-identical to the CPU path)",
+                   "parallelism": f"image-sharded x{world}, {S} HIP streams x {B // S} images per GPU" +
+                                  (", RCCL keypoint gather one step behind" if gathering else "")},
+        "output_verified": bool(verified) and not failed,
+        "output_verified_seeds": verified,
+        "keypoints_per_s": round(kp_total_step * a.steps / dt, 1),
+        "keypoints_per_step": int(kp_total_step),
+        "roofline": roof,
+        "roofline_octaves_2d_tiles": roof_gather,
+        "pyramid": {"ms_per_step": round(pyr_ms / a.steps, 3),
+                    "algorithmic_GBs": round(pyr_bytes / (pyr_ms * 1e-3) / 1e9, 1) if pyr_ms else None,
+                    "note": "B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes), SURVEY.md 8(d)"},
+        "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in stats.items()},
+        "serial_leg": {"ms_per_step": round(pdt / a.steps * 1e3, 3),
+                       "Mpix_per_s": round(mpix / pdt, 2),
+                       "note": "one context, the whole batch on one stream, HIP events around every "
+                               "stage (SIFT_FLAG_PROFILE, no graph): the source of stages_ms_per_step, "
+                               "roofline and descriptor; value is the streams leg (graph replay, no "
+                               "events)"},
+    })
+    if failed:
+        out["output_failed_seeds"] = failed
+    if gathering:
+        out["gather"] = res["gather"]
+    d = stats.get("descriptor")
+    if d:
+        out["descriptor"] = {"ms_per_step": round(d["ms"] / a.steps, 3),
+                             "keypoints_per_s_kernel": round(kp_total_step / world * a.steps /
+                                                             (d["ms"] * 1e-3), 1),
+                             "roofline": descriptor_roofline(tr, d)}
+    return out
+
+
+def fast_block(a, world, B, R, C, fast_res, tr):
+    (fdt, _, fkp), fast_prof = fast_res
+    fst = fast_prof[1]
+    mpix = world * B * R * C * a.steps / 1e6
+    pf = fst.get("pyramid_fast", {"ms": 0.0, "bytes": 0.0, "launches": 0})
+    gbs = pf["bytes"] / (pf["ms"] * 1e-3) / 1e9 if pf["ms"] else 0.0
+    traffic, tsrc = traffic_of(tr, "pyr_fast_kernel")
+    fm = {
+        "value": round(mpix / fdt, 2), "unit": "Mpix/s", "ms_per_step": round(fdt / a.steps * 1e3, 3),
+        "keypoints_per_s": round(fkp * a.steps / fdt, 1), "keypoints_per_step": int(fkp),
+        "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in fst.items()},
+        "note": "the exact leg's stream split (--streams), graph replay; SIFT_FLAG_FAST: separable row/column "
+                "Gaussian pyramid (pyramid_fast.hip) in front of the same exact DoG/extrema/orientation/"
+                "descriptor kernels; not bit-exact (float rounding of the pyramid), keypoint/descriptor "
+                "match rates vs the CPU path are in tests/test_gpu_fast.py"}
+    roof = {
+        "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "traffic_algorithmic": round(pf["bytes"] / max(pf["launches"], 1)),
+        "traffic_source": tsrc, "kernel": "pyr_fast_kernel",
+        "avg_launch_ms": round(pf["ms"] / max(pf["launches"], 1), 4),
+        "pyramid_ms_per_step": round(pf["ms"] / a.steps, 4),
+        "note": "algorithmic bytes B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes, "
+                "SURVEY.md 8(d)) over the per-octave launches of one step, / their summed "
+                "HIP-event time; north_star target frac >= 0.6"}
+    return fm, roof
+
+
+def match_block(a, world, match):
+    pairs = match["n_query"] * match["n_train"]
+    lane_ops = match["flops"] / (match["ms"] * 1e-3) / 1e12 if match["ms"] else 0.0
+    m = {
+        "metric": "knnMatch(k=2) L1 distance pairs/s, image 1 vs image 0 of the batch",
+        "value": round(pairs / (match["ms"] * 1e-3) / 1e9, 3) if match["ms"] else None,
+        "unit": "Gpairs/s", "ms": round(match["ms"], 4),
+        "n_query": match["n_query"], "n_train": match["n_train"],
+        "roofline": {"bound": "valu", "achieved": round(lane_ops, 2), "peak": VALU_OP_PEAK_T,
+                     "unit": "Tlane-op/s", "frac": round(lane_ops / VALU_OP_PEAK_T, 4),
+                     "kernel": "knn_l1_kernel",
+                     "note": "2 VALU lane-ops (v_sub, v_add |x|) per descriptor element per pair; "
+                             "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"},
+        "note": "SURVEY 8(f) f2 (src/main.cpp:25-27); bit-exact vs oracle/match.py"}
+    if world == 1 and not a.no_cpu_baseline:
+        m["cpu_baseline"] = match_cpu_baseline(match)
+    return m
+
+
+def assemble(a, world, env_shape, res, cpu, errors):
+    """The one JSON line.  Every optional block is built under its own guard:
+    a failure there becomes {"error": ...} and the headline fields stay."""
+    B, R, C, S = env_shape
+    tr = load_traffic()
+    out = {"metric": METRIC}
+    if res.get("exact") is not None:
+        out.update(exact_block(a, world, B, R, C, S, res["exact"], tr))
+    if res.get("fast") is not None:
+        fb = guarded(errors, "fast_block", fast_block, a, world, B, R, C, res["fast"], tr)
+        if fb is not None:
+            out["fast_mode"], out["roofline_pyramid_fast"] = fb
+    if res.get("match") is not None:
+        mb = guarded(errors, "match_block", match_block, a, world, res["match"])
+        if mb is not None:
+            out["match"] = mb
+    if res.get("single") is not None:
+        out["single_image"] = res["single"]
+    if res.get("eightk") is not None:
+        out["image_8k"] = res["eightk"]
+    if cpu:
+        out.update(cpu)
+        cb = cpu.get("cpu_baseline")
+        if cb and "value" in out:
+            out["speedup_vs_cpu_1thread"] = {"Mpix/s": round(out["value"] / cb["value"], 1),
+                                             "keypoints/s": round(out["keypoints_per_s"] / cb["keypoints_per_s"], 1)}
+        if cb and res.get("single") is not None:
+            res["single"]["speedup_vs_cpu_1thread_keypoints_per_s"] = round(
+                res["single"]["keypoints_per_s"] / cb["keypoints_per_s"], 1)
+    for name in errors:
+        block = {"fast": "fast_mode", "fast_block": "fast_mode", "match": "match", "match_block": "match",
+                 "single": "single_image", "eightk": "image_8k"}.get(name)
+        if block and block not in out:
+            out[block] = {"error": errors[name]}
+    if errors:
+        out["leg_errors"] = dict(errors)
+    return out
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    errors = {}
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline and a.only is None:
+        # before this process touches the GPU: the image-parallel leg starts
+        # child processes
+        cpu = cpu_legs(a, errors)
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    env = Env(a, world, rank)
+    want = (lambda leg_name: a.only in (None, leg_name))
+    res = {}
+    if want("exact"):
+        res["exact"] = run_exact(env)   # the headline: not guarded
+    if not a.no_fast and want("fast"):
+        res["fast"] = guarded(errors, "fast", run_fast, env)
+    if not (a.no_match or rank != 0 or env.B < 2 or res.get("exact") is None):
+        res["match"] = guarded(errors, "match", run_match, env)
+    if rank == 0 and world == 1 and not a.no_single and want("single"):
+        res["single"] = guarded(errors, "single", single_image_leg, env.R, env.C, a.steps, a.warmup)
+    if rank == 0 and world == 1 and not a.no_8k and want("8k"):
+        res["eightk"] = guarded(errors, "eightk", eightk_leg, a.steps, a.warmup)
     if rank == 0:
-        tr = load_traffic()
-        out = {"metric": METRIC}
-        if exact is not None:
-            dt, _, kp_total_step = exact
-            pdt, stats, _ = prof   # stage times / rooflines: the serial profiled leg
-            mpix = world * B * R * C * a.steps / 1e6
-            value = mpix / dt
-            # roofline of the dominant kernel: the exact octave blur -- octave 0
-            # in scatter form (blur_sym_kernel) when the library chose it for
-            # this launch size, the 2-D tiles (blur_octave_kernel) otherwise
-            def blur_roof(stage, kernel):
-                bo = stats.get(stage)
-                if not bo or not bo["launches"]:
-                    return None
-                per_launch_ms = bo["ms"] / bo["launches"]
-                tflops = (bo["flops"] / bo["launches"]) / (per_launch_ms * 1e-3) / 1e12 if per_launch_ms else 0.0
-                traffic, tsrc = traffic_of(tr, kernel)
-                r = {"bound": "valu", "achieved": round(tflops, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "traffic_algorithmic": round(bo["bytes"] / bo["launches"]),
-                     "traffic_source": tsrc, "kernel": kernel, "launches_per_step": bo["launches"] // a.steps,
-                     "avg_launch_ms": round(per_launch_ms, 4),
-                     "valu_issue_frac": valu_issue_frac(tr, kernel, per_launch_ms),
-                     "note": "exact-mode 2-D blur is fp32-VALU bound, no MFMA; peak = the fp32 vector peak "
-                             "(FMA counted as 2 flops); flops = 2 x taps per launch, algorithmic (the "
-                             "reference's chain: one multiply + one add per tap, FMA forbidden by the parity "
-                             "contract), 4 scales x the whole batch; traffic = HBM bytes per launch from the "
-                             "committed rocprofv3 PMC pass (calibrated FETCH_SIZE/WRITE_SIZE); valu_issue_frac = "
-                             "SQ_INSTS_VALU per launch (same PMC pass) / launch time / the wave64 VALU issue peak "
-                             "(256 CU x 4 SIMD x 2.4 GHz / 2 cycles)"}
-                if kernel == "blur_sym_kernel":
-                    r["note"] += ("; scatter form: K[a][b] = K[-a][b], so each multiply serves kernel rows +a "
-                                  "and -a of two outputs -- (2w+1)(w+1) multiplies + (2w+1)^2 adds per output "
-                                  "instead of 2(2w+1)^2, same chain, bit-exact -- which is why frac can pass 0.5")
-                return r
-            sym_used = "blur_octave_sym" in stats
-            roof = blur_roof("blur_octave_sym", "blur_sym_kernel") if sym_used else \
-                blur_roof("blur_octave", "blur_octave_kernel")
-            roof_gather = blur_roof("blur_octave", "blur_octave_kernel") if sym_used else None
-            pyr_ms = sum(stats[k]["ms"] for k in ("blur_base", "blur_octave", "blur_octave_sym", "decimate", "dog")
-                         if k in stats)
-            pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
-            out.update({
-                "value": round(value, 2),
-                "unit": "Mpix/s",
-                "n_gpus": world,
-                "steps": a.steps,
-                "warmup": a.warmup,
-                "ms_per_step": round(dt / a.steps * 1e3, 3),
-                "higher_is_better": True,
-                "scaling": "weak",
-                "vs_baseline": None,
-                "dtype": "f32",
-                "data": "synthetic: integer-exact 1920x1080 textures (SURVEY.md 8(d) d2) generated on device",
-                "config": {"workload": f"configs[2]: batch of {B} x {C}x{R} synthetic grayscale per GPU "
-                                       f"(N=8 x 64 = configs[3]), {a.octaves} octaves x 5 scales, exact mode",
-                           "global_batch": world * B, "rows": R, "cols": C, "octaves": a.octaves,
-                           "mode": "exact (bit-identical to the CPU path)",
-                           "parallelism": f"image-sharded x{world}, {S} HIP streams x {B // S} images per GPU" +
-                                          (", RCCL keypoint gather one step behind" if gathering else "")},
-                "output_verified": bool(verified) and not failed,
-                "output_verified_seeds": verified,
-                "keypoints_per_s": round(kp_total_step * a.steps / dt, 1),
-                "keypoints_per_step": int(kp_total_step),
-                "roofline": roof,
-                "roofline_octaves_2d_tiles": roof_gather,
-                "pyramid": {"ms_per_step": round(pyr_ms / a.steps, 3),
-                            "algorithmic_GBs": round(pyr_bytes / (pyr_ms * 1e-3) / 1e9, 1) if pyr_ms else None,
-                            "note": "B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes), SURVEY.md 8(d)"},
-                "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in stats.items()},
-                "serial_leg": {"ms_per_step": round(pdt / a.steps * 1e3, 3),
-                               "Mpix_per_s": round(mpix / pdt, 2),
-                               "note": "one context, the whole batch on one stream, HIP events around every "
-                                       "stage (SIFT_FLAG_PROFILE, no graph): the source of stages_ms_per_step, "
-                                       "roofline and descriptor; value is the streams leg (graph replay, no "
-                                       "events)"},
-            })
-            if failed:
-                out["output_failed_seeds"] = failed
-            if gathering:
-                out["gather"] = {"steps_gathered": gathered["steps"],
-                                 "keypoints_gathered_per_step": gathered["keypoints"] / max(gathered["steps"], 1)}
-            d = stats.get("descriptor")
-            if d:
-                out["descriptor"] = {"ms_per_step": round(d["ms"] / a.steps, 3),
-                                     "keypoints_per_s_kernel": round(kp_total_step / world * a.steps /
-                                                                     (d["ms"] * 1e-3), 1),
-                                     "roofline": descriptor_roofline(tr, d)}
-        if fast is not None:
-            fdt, _, fkp = fast
-            fst = fast_prof[1]
-            mpix = world * B * R * C * a.steps / 1e6
-            pf = fst.get("pyramid_fast", {"ms": 0.0, "bytes": 0.0, "launches": 0})
-            gbs = pf["bytes"] / (pf["ms"] * 1e-3) / 1e9 if pf["ms"] else 0.0
-            traffic, tsrc = traffic_of(tr, "pyr_fast_kernel")
-            out["fast_mode"] = {
-                "value": round(mpix / fdt, 2), "unit": "Mpix/s", "ms_per_step": round(fdt / a.steps * 1e3, 3),
-                "keypoints_per_s": round(fkp * a.steps / fdt, 1), "keypoints_per_step": int(fkp),
-                "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in fst.items()},
-                "note": "the exact leg's stream split (--streams), graph replay; SIFT_FLAG_FAST: separable row/column Gaussian "
-                        "pyramid (pyramid_fast.hip) in front of "
-                        "the same exact DoG/extrema/orientation/descriptor kernels; not bit-exact (float "
-                        "rounding of the pyramid), keypoint/descriptor match rates vs the CPU path are in "
-                        "tests/test_gpu_fast.py"}
-            out["roofline_pyramid_fast"] = {
-                "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_algorithmic": round(pf["bytes"] / max(pf["launches"], 1)),
-                "traffic_source": tsrc, "kernel": "pyr_fast_kernel",
-                "avg_launch_ms": round(pf["ms"] / max(pf["launches"], 1), 4),
-                "pyramid_ms_per_step": round(pf["ms"] / a.steps, 4),
-                "note": "algorithmic bytes B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes, "
-                        "SURVEY.md 8(d)) over the five per-octave launches of one step, / their summed "
-                        "HIP-event time; north_star target frac >= 0.6"}
-        if match is not None:
-            pairs = match["n_query"] * match["n_train"]
-            lane_ops = match["flops"] / (match["ms"] * 1e-3) / 1e12 if match["ms"] else 0.0
-            out["match"] = {
-                "metric": "knnMatch(k=2) L1 distance pairs/s, image 1 vs image 0 of the batch",
-                "value": round(pairs / (match["ms"] * 1e-3) / 1e9, 3) if match["ms"] else None,
-                "unit": "Gpairs/s", "ms": round(match["ms"], 4),
-                "n_query": match["n_query"], "n_train": match["n_train"],
-                "roofline": {"bound": "valu", "achieved": round(lane_ops, 2), "peak": VALU_OP_PEAK_T,
-                             "unit": "Tlane-op/s", "frac": round(lane_ops / VALU_OP_PEAK_T, 4),
-                             "kernel": "knn_l1_kernel",
-                             "note": "2 VALU lane-ops (v_sub, v_add |x|) per descriptor element per pair; "
-                                     "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"},
-                "note": "SURVEY 8(f) f2 (src/main.cpp:25-27); bit-exact vs oracle/match.py"}
-            if world == 1 and not a.no_cpu_baseline:
-                out["match"]["cpu_baseline"] = match_cpu_baseline(match)
-        if single is not None:
-            out["single_image"] = single
-        if eightk is not None:
-            out["image_8k"] = eightk
-        if cpu is not None:
-            out.update(cpu)
-            cb = cpu["cpu_baseline"]
-            if exact is not None:
-                out["speedup_vs_cpu_1thread"] = {"Mpix/s": round(out["value"] / cb["value"], 1),
-                                                 "keypoints/s": round(out["keypoints_per_s"] / cb["keypoints_per_s"], 1)}
-            if single is not None:
-                single["speedup_vs_cpu_1thread_keypoints_per_s"] = round(
-                    single["keypoints_per_s"] / cb["keypoints_per_s"], 1)
-        if a.profile_json and prof is not None:
+        out = assemble(a, world, (env.B, env.R, env.C, env.S), res, cpu, errors)
+        if a.profile_json and res.get("exact") is not None:
             with open(a.profile_json, "w") as f:
-                json.dump(prof[1], f, indent=1)
+                json.dump(res["exact"]["prof"][1], f, indent=1)
         print(json.dumps(out), flush=True)
-    for p in parts + [serial]:
-        p.close()
+    env.close()
     if world > 1:
         dist.destroy_process_group()
 

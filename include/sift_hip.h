@@ -92,6 +92,13 @@ int sift_sync(sift_ctx* ctx);
  * 1080p image.  Reallocates the workspace (synchronises). */
 int sift_set_candidate_capacity(sift_ctx* ctx, int per_image);
 const char* sift_version(void);
+/* hipGraph cache counters of this context: sequences captured, cached
+ * executables patched in place (hipGraphExecUpdate: same shape, other
+ * buffers) and executables instantiated.  The cache holds 4 shapes; a call
+ * whose shape (batch, dims, strides, kp_cap, octaves, flags) and buffers both
+ * match a cached entry replays it with no capture at all, so callers that can
+ * keep their device buffers stable (or rotate among a few) pay no capture. */
+int sift_graph_stats(const sift_ctx* ctx, long long* captures, long long* updates, long long* instantiations);
 
 /* ---- layout helpers ----------------------------------------------------- */
 /* Octave shapes: octave o+1 = Size(cols/2, rows/2) of octave o (src/sift.cpp:254). */

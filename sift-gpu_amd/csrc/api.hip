@@ -156,11 +156,13 @@ struct sift_ctx {
   // hipGraph cache of compute sequences (one per argument set; SIFT_FLAG_NO_GRAPH,
   // _PROFILE and _VERBOSE run the launches directly)
   struct GraphEntry {
-    std::vector<char> key;
+    std::vector<char> key;   // everything that shapes the sequence (dims, batch, flags, ...)
+    std::vector<char> ptrs;  // the caller's buffers baked into the kernel arguments
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
   };
   std::vector<GraphEntry> graphs;
+  long long graph_captures = 0, graph_updates = 0, graph_instantiations = 0;  // sift_graph_stats
   size_t match_cap = 0;
   // profiling
   std::vector<StageRec> recs;
@@ -445,22 +447,25 @@ bool graphs_enabled(const sift_ctx* c) {
 }
 
 // Runs body() on the context stream: replayed from a cached hipGraph when one
-// was captured for the same key, captured now otherwise (direct launches if
-// graphs are off or capture fails).
+// was captured for the same key and buffers; captured now otherwise (direct
+// launches if graphs are off or capture fails).  A caller whose buffers move
+// between calls (a caching allocator, a ring of output slots) with the same
+// shape gets the new capture patched into the cached executable with
+// hipGraphExecUpdate -- no re-instantiation -- so a rotating set of buffers
+// does not thrash the 4-entry cache.
 template <typename F>
-int run_graphed(sift_ctx* c, const std::vector<char>& key, F&& body) {
+int run_graphed(sift_ctx* c, const std::vector<char>& key, const std::vector<char>& ptrs, F&& body) {
   if (!graphs_enabled(c)) {
     body();
     HIP_TRY(c, hipGetLastError());
     return SIFT_OK;
   }
   for (size_t i = 0; i < c->graphs.size(); ++i)
-    if (c->graphs[i].key == key) {
+    if (c->graphs[i].key == key && c->graphs[i].ptrs == ptrs) {
       HIP_TRY(c, hipGraphLaunch(c->graphs[i].exec, c->stream));
       return SIFT_OK;
     }
-  sift_ctx::GraphEntry e;
-  e.key = key;
+  hipGraph_t g = nullptr;
   if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     (void)hipGetLastError();
     body();
@@ -469,15 +474,44 @@ int run_graphed(sift_ctx* c, const std::vector<char>& key, F&& body) {
   }
   body();
   const hipError_t le = hipGetLastError();
-  const hipError_t ce = hipStreamEndCapture(c->stream, &e.graph);
-  if (le != hipSuccess || ce != hipSuccess || !e.graph ||
-      hipGraphInstantiate(&e.exec, e.graph, nullptr, nullptr, 0) != hipSuccess) {
-    if (e.graph) (void)hipGraphDestroy(e.graph);
+  const hipError_t ce = hipStreamEndCapture(c->stream, &g);
+  if (le != hipSuccess || ce != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();
     body();  // capture failed: nothing ran, launch directly
     HIP_TRY(c, hipGetLastError());
     return SIFT_OK;
   }
+  c->graph_captures++;
+  // same shape, other buffers: update the cached executable in place
+  for (size_t i = 0; i < c->graphs.size(); ++i) {
+    sift_ctx::GraphEntry& e = c->graphs[i];
+    if (e.key != key) continue;
+    hipGraphNode_t err_node = nullptr;
+    hipGraphExecUpdateResult res;
+    if (hipGraphExecUpdate(e.exec, g, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess) {
+      (void)hipGraphDestroy(e.graph);
+      e.graph = g;
+      e.ptrs = ptrs;
+      c->graph_updates++;
+      HIP_TRY(c, hipGraphLaunch(e.exec, c->stream));
+      return SIFT_OK;
+    }
+    (void)hipGetLastError();
+    break;  // not updatable: instantiate a new executable below
+  }
+  sift_ctx::GraphEntry e;
+  e.key = key;
+  e.ptrs = ptrs;
+  e.graph = g;
+  if (hipGraphInstantiate(&e.exec, e.graph, nullptr, nullptr, 0) != hipSuccess) {
+    (void)hipGraphDestroy(e.graph);
+    (void)hipGetLastError();
+    body();
+    HIP_TRY(c, hipGetLastError());
+    return SIFT_OK;
+  }
+  c->graph_instantiations++;
   if (c->graphs.size() >= 4) {
     (void)hipGraphExecDestroy(c->graphs.front().exec);
     (void)hipGraphDestroy(c->graphs.front().graph);
@@ -527,6 +561,14 @@ void verbose_phase(sift_ctx* c, const char* what, hipEvent_t a, hipEvent_t b) {
 
 extern "C" {
 
+int sift_graph_stats(const sift_ctx* c, long long* captures, long long* updates, long long* instantiations) {
+  if (!c || !captures || !updates || !instantiations) return SIFT_E_INVALID;
+  *captures = c->graph_captures;
+  *updates = c->graph_updates;
+  *instantiations = c->graph_instantiations;
+  return SIFT_OK;
+}
+
 const char* sift_version(void) { return "sift-hip 0.2 (gfx950; exact + SIFT_FLAG_FAST separable pyramid)"; }
 
 int sift_octave_shapes(int rows, int cols, int n_octaves, int* orows, int* ocols) {
@@ -556,6 +598,9 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
                     sift_ctx** out) {
   if (!out || max_rows < 1 || max_cols < 1 || max_batch < 1) return SIFT_E_INVALID;
   *out = nullptr;
+  // descriptor.hip gathers with 32-bit element offsets inside one plane
+  // (row * pitch + col): an octave-0 plane must stay below 2^31 elements
+  if ((long long)max_rows * round_up(max_cols, 16) >= (1ll << 31)) return SIFT_E_SIZE;
   if (hipSetDevice(device) != hipSuccess) return SIFT_E_HIP;
   sift_ctx* c = new sift_ctx();
   c->device = device;
@@ -779,21 +824,21 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
     HIP_TRY(c, hipGetLastError());
     return SIFT_OK;
   }
-  std::vector<char> key;
+  std::vector<char> key, ptrs;
   key_put(key, 1);  // sequence id
-  key_put(key, d_imgs);
   key_put(key, batch);
   key_put(key, rows);
   key_put(key, cols);
   key_put(key, row_stride);
   key_put(key, img_stride);
-  key_put(key, d_kpts);
-  key_put(key, d_desc);
   key_put(key, kp_cap);
-  key_put(key, d_img_offsets);
   key_put(key, c->n_oct);
   key_put(key, c->flags);
-  return run_graphed(c, key, [&]() {
+  key_put(ptrs, d_imgs);
+  key_put(ptrs, d_kpts);
+  key_put(ptrs, d_desc);
+  key_put(ptrs, d_img_offsets);
+  return run_graphed(c, key, ptrs, [&]() {
     enqueue_pyramid(c, L, src, batch, false);
     enqueue_detect(c, L, batch, d_kpts, kp_cap, d_img_offsets, true);
     enqueue_desc(c, L, d_kpts, d_img_offsets, batch, kp_cap, d_desc, 0, true);

@@ -336,6 +336,14 @@ struct SymArgs {
   int chunk[4];        // output rows per wave, per slot
 };
 
+// Wave-scope ordering of LDS accesses across lanes: no instruction, but the
+// compiler may not move loads or stores across it.
+__device__ __forceinline__ void wave_sync_b() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One wave: output columns [x0, x0 + 64) x rows [y0, y1) of one plane.
 template <int T>
 __device__ __forceinline__ void sym_walk(const SymArgs& A, int slot, int local, float* __restrict__ ring) {
@@ -379,6 +387,10 @@ __device__ __forceinline__ void sym_walk(const SymArgs& A, int slot, int local, 
   int r0 = max(y0 - W, 0);
   fetch(r0);
   stage(0);
+  // Lanes read ring words other lanes wrote: order the stores before every
+  // later read and every read before the next reuse of that ring half (each
+  // wave_sync sits between the reads of a half and its next stage).
+  wave_sync_b();
   int h = 0;
   for (; r0 < y1 + W; r0 += R) {
     fetch(r0 + R);  // next step's rows, in flight during this step
@@ -416,6 +428,7 @@ __device__ __forceinline__ void sym_walk(const SymArgs& A, int slot, int local, 
     for (int k = NA - R; k < NA; ++k) acc[k] = 0.f;
     h ^= 1;
     stage(h);
+    wave_sync_b();
   }
 }
 

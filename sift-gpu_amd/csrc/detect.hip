@@ -444,6 +444,7 @@ __global__ __launch_bounds__(64) void extrema_walk_kernel(WalkArgs A) {
   load(y0 + 1, vc, hc);
   // ring slot of row r: (r - y0 + 1) % 3, i.e. set a <-> slot 0, b <-> 1, c <-> 2
   auto step = [&](int r, float (&v)[6], float (&h)[6], int sr) {
+    wave_sync();  // the previous process() read slot sr (row r - 3) at other lanes' columns
     put(sr, r, v, h);
     wave_sync();
     if (r + 3 <= y1) load(r + 3, v, h);

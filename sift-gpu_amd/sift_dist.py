@@ -74,6 +74,12 @@ class GatherPipeline:
         self.done = [None] * slots        # transfers of this slot finished (device event)
         self.ready = [None] * slots       # compute of this slot finished (device event)
         self.side = torch.cuda.Stream() if self.cuda else None
+        # evidence for the bench line at N > 1: what this rank received per
+        # peer and how long the side stream's transfers took
+        self.gathers = 0
+        self.recv_counts = [0] * self.world   # records received from each rank (dst only)
+        self.sent_records = 0                 # records this rank sent (rank != dst)
+        self._spans = []                      # (start, end) device events of each transfer group
 
     # -- compute side ---------------------------------------------------------
     def wait_slot(self, s: int):
@@ -105,6 +111,13 @@ class GatherPipeline:
         offs = [allo[r][:self.batches[r] + 1] for r in range(self.world)]
         counts = [min(int(o[-1]), self.cap) for o in offs]   # host ints: no device read
         recv_k, recv_d = {}, {}
+        self.gathers += 1
+        if self.rank == self.dst:
+            for r in range(self.world):
+                if r != self.dst:
+                    self.recv_counts[r] += counts[r]
+        else:
+            self.sent_records += counts[self.rank]
 
         def post():
             # receive buffers are allocated here, on the stream that uses them
@@ -129,10 +142,13 @@ class GatherPipeline:
         if self.cuda:
             self.side.wait_event(self.ready[s])
             with torch.cuda.stream(self.side):
+                t0 = torch.cuda.Event(enable_timing=True)
+                t0.record(self.side)
                 post()
-                ev = torch.cuda.Event()
+                ev = torch.cuda.Event(enable_timing=True)
                 ev.record(self.side)
                 self.done[s] = ev
+                self._spans.append((t0, ev))
         else:
             post()
         if self.rank != self.dst:
@@ -150,6 +166,23 @@ class GatherPipeline:
     def sync(self):
         if self.cuda:
             self.side.synchronize()
+
+    def reset_stats(self):
+        self.gathers, self.sent_records = 0, 0
+        self.recv_counts = [0] * self.world
+        self._spans = []
+
+    def stats(self) -> dict:
+        """Per-rank gather evidence since the last reset_stats(); call after
+        sync().  transfer_ms = summed device time of the side stream's
+        transfer groups (each from its start, i.e. after the step's compute,
+        to the last receive/send completing)."""
+        ms = None
+        if self.cuda and self._spans:
+            ms = sum(a.elapsed_time(b) for a, b in self._spans)
+        return {"backend": dist.get_backend(), "world_size": self.world, "rank": self.rank,
+                "gathers": self.gathers, "received_records_per_rank": list(self.recv_counts),
+                "sent_records": self.sent_records, "transfer_ms": ms}
 
 
 class PipelinedSteps:
@@ -192,11 +225,17 @@ def gather_keypoints(kpts: torch.Tensor, offs: torch.Tensor, dst: int = 0,
                      desc: torch.Tensor | None = None, batches: list[int] | None = None):
     """One-shot gather of every rank's keypoints (and per-image offsets,
     optionally descriptors) to rank `dst` (GatherPipeline with one slot,
-    waited for).  batches: every rank's batch size; default: all ranks have
-    this rank's len(offs) - 1 (only valid for equal shards)."""
+    waited for).  batches: every rank's batch size; default: every rank's
+    len(offs) - 1, exchanged with one all_gather on the metadata group (shards
+    may be uneven: sift_dist.shard gives them so whenever total % world != 0)."""
     world = dist.get_world_size()
     b = offs.shape[0] - 1
-    batches = batches or [b] * world
+    if batches is None:
+        mine = torch.tensor([b], dtype=torch.int64)
+        allb = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allb, mine, group=_meta_group())
+        batches = [int(x.item()) for x in allb]
+    assert len(batches) == world and batches[dist.get_rank()] == b, (batches, b)
     pipe = GatherPipeline(batches, kpts.shape[0], dst, slots=1)
     pipe.mark(0, offs)
     out = pipe.gather(0, kpts, desc)

@@ -84,6 +84,8 @@ def lib():
             "sift_sync": (ip, [vp]),
             "sift_set_candidate_capacity": (ip, [vp, ip]),
             "sift_version": (ctypes.c_char_p, []),
+            "sift_graph_stats": (ip, [vp, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
+                                      ctypes.POINTER(ctypes.c_longlong)]),
             "sift_octave_shapes": (ip, [ip, ip, ip, pint, pint]),
             "sift_packed_size": (sz, [ip, ip, ip, ip]),
             "sift_detect_compute": (ip, [vp, fp, ip, ip, sz, vp, fp, ip, pint]),
@@ -197,6 +199,12 @@ class Context:
 
     def sync(self):
         self._check("sift_sync", self._L.sift_sync(self.h))
+
+    def graph_stats(self):
+        """(captures, in-place updates, instantiations) of the context's hipGraph cache."""
+        v = [ctypes.c_longlong(0) for _ in range(3)]
+        self._check("sift_graph_stats", self._L.sift_graph_stats(self.h, *[ctypes.byref(x) for x in v]))
+        return tuple(x.value for x in v)
 
     def set_candidate_capacity(self, per_image: int):
         self._check("sift_set_candidate_capacity", self._L.sift_set_candidate_capacity(self.h, per_image))

@@ -110,3 +110,13 @@ def test_pack_split_roundtrip(siftgpu):
     assert all(np.array_equal(a, b) for a, b in zip(planes, back))
     with pytest.raises(ValueError):
         siftgpu.pack_planes(planes[:-1], 37, 53, 3, 5)
+
+
+def test_ctx_create_rejects_planes_over_2g_elements(siftgpu):
+    """descriptor.hip gathers with 32-bit element offsets inside a plane:
+    an octave-0 plane of 2^31 or more elements is refused up front
+    (SIFT_E_SIZE), before any device call."""
+    L = siftgpu.lib()
+    h = ctypes.c_void_p()
+    assert L.sift_ctx_create(0, 46341, 46352, 1, 0, ctypes.byref(h)) == siftgpu.SIFT_E_SIZE and not h.value
+    assert L.sift_ctx_create(0, 1 << 16, 1 << 15, 1, 0, ctypes.byref(h)) == siftgpu.SIFT_E_SIZE

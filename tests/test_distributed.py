@@ -69,6 +69,10 @@ def _worker(rank, world, port, q):
         out = sdist.gather_keypoints(kp, offs_u, dst=0, batches=batches)
         if rank == 0:
             q.put(([k.shape[0] for k in out[0]], [o.tolist() for o in out[1]]))
+        # the same without `batches`: the shard sizes are exchanged
+        out = sdist.gather_keypoints(kp, offs_u, dst=0)
+        if rank == 0:
+            q.put(([k.shape[0] for k in out[0]], [o.tolist() for o in out[1]]))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -108,6 +112,14 @@ def _pipeline_worker(rank, world, port, q):
                 d[:len(desc)] = desc
             runner.step(compute)
         runner.flush()
+        st = pipe.stats()   # the bench line's N > 1 evidence
+        n1 = sum(int(_fake_step(1, step, cap)[0][-1]) for step in range(5))
+        ok_stats = st["gathers"] == 5 and st["world_size"] == world and st["backend"] == "gloo"
+        if rank == 0:
+            ok_stats = ok_stats and st["received_records_per_rank"] == [0, n1] and st["sent_records"] == 0
+        else:
+            ok_stats = ok_stats and st["sent_records"] == n1
+        assert ok_stats, st
         if rank == 0:
             ok = sorted(got) == list(range(5))
             for step in range(5):
@@ -202,6 +214,7 @@ def test_gather_keypoints_world2():
         ks, offs, ds = q.get(timeout=120)
         shapes = q.get(timeout=120)
         uneven = q.get(timeout=120)
+        uneven_default = q.get(timeout=120)
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -214,6 +227,7 @@ def test_gather_keypoints_world2():
         assert np.all(ds[r] == r + 1)
     assert shapes == [4, 0]
     assert uneven == ([4, 5], [[0, 1, 4], [0, 1, 2, 5]])
+    assert uneven_default == uneven
 
 
 def test_pipelined_parts_world2():

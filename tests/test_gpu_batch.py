@@ -192,3 +192,42 @@ def test_batch_keypoint_capacity(siftgpu, oracle):
         assert_bits_equal(kpts.cpu().numpy().view(np.uint8).reshape(cap, 28), kp_bytes(k0[:cap]), "first kp_cap")
         assert_bits_equal(desc.cpu().numpy(), d0[:cap], "first kp_cap descriptors")
         ctx.sync()  # reported once
+
+
+def test_graph_cache_rotating_buffers(siftgpu, oracle):
+    """a caller rotating among more output buffers than the graph
+    cache holds (6 slots, 4 entries) with one shape.  Each new buffer set
+    patches the cached executable in place (hipGraphExecUpdate) instead of
+    instantiating; every call's output is the CPU path's, in its own slot,
+    and replays of earlier slots still land in those slots."""
+    import torch
+    B, r, c = 3, 96, 128
+    ref = [oracle.sift(oracle.synth_image(70 + b, r, c)) for b in range(B)]
+    n = [len(k) for k, _ in ref]
+    with siftgpu.Context(r, c, B, device=0) as ctx:
+        imgs = torch.empty((B, r, c), dtype=torch.float32, device="cuda")
+        ctx.synth_images(imgs.data_ptr(), B, r, c, c, r * c, seed_base=70)
+        cap = 4 * sum(n)
+        slots = [(torch.full((cap, 7), -1, dtype=torch.int32, device="cuda"),
+                  torch.full((cap, 128), -1.0, dtype=torch.float32, device="cuda"),
+                  torch.full((B + 1,), -1, dtype=torch.int32, device="cuda")) for _ in range(6)]
+        order = [0, 1, 2, 3, 4, 5, 0, 3, 5, 1]
+        for i in order:
+            k, d, o = slots[i]
+            k.fill_(-1)
+            d.fill_(-1.0)
+            o.fill_(-1)
+            ctx.detect_compute_batch(imgs.data_ptr(), B, r, c, c, r * c, k.data_ptr(), d.data_ptr(), cap,
+                                     o.data_ptr())
+            ctx.sync()
+            oo = o.cpu().numpy()
+            kk = k.cpu().numpy().view(np.uint8).reshape(cap, 28)
+            dd = d.cpu().numpy()
+            for b in range(B):
+                assert oo[b + 1] - oo[b] == n[b], f"slot {i} image {b}"
+                assert_bits_equal(kk[oo[b]:oo[b + 1]], kp_bytes(ref[b][0]), f"slot {i} image {b} keypoints")
+                assert_bits_equal(dd[oo[b]:oo[b + 1]], ref[b][1], f"slot {i} image {b} descriptors")
+            assert np.all(kk[oo[B]:].view(np.int32) == -1), f"slot {i}: writes past the total"
+        caps, upd, inst = ctx.graph_stats()
+    assert inst == 1, (caps, upd, inst)          # one shape: one executable
+    assert upd == caps - 1 == len(order) - 1, (caps, upd, inst)  # every other call patched it
