@@ -133,6 +133,7 @@ struct sift_ctx {
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
   std::vector<char> fast_taps;    // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip), passed by value
+  bool fast_pair = true;          // SIFT_FLAG_FAST via pyramid_pair.hip (round 3)
   size_t coef_gen_cap = 0;
   int wsz[4] = {0, 0, 0, 0};
   int w_base = 0;
@@ -317,8 +318,21 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
     for (int o = 0; o < L.n_oct; ++o) {
       const double px = plane_px(L, o) * batch;
       const double taps = 2.0 * (9 + 17 + 25 + 37) + (o == 0 ? 2.0 * 9 : 0.0);
-      StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-      launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
+      if (c->fast_pair) {
+        // pyramid_pair.hip: octave o-1's launch wrote plane 0 of octave o when
+        // it is an exact half; otherwise decimate first (plane 0
+        // is one of the five plane writes, the decimation's read is not
+        // algorithmic, so it is outside the pyramid stage's bytes)
+        if (o > 0 && !pyramid_pair_fuses(L, o)) {
+          StageScope s(c, ST_DECIMATE, 0, 8.0 * px);
+          launch_decimate(st, L, o, c->d_gpyr, batch);
+        }
+        StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
+        launch_pyramid_pair(st, L, o, c->d_gpyr, src, batch);
+      } else {
+        StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
+        launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
+      }
     }
     if (with_dog)
       for (int o = 0; o < L.n_oct; ++o) {
@@ -667,6 +681,12 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   }
   c->fast_taps.resize(fast_coefs_size());
   if (fast_coefs_host(sb, sig_f, c->fast_taps.data()) != 0) return bail(SIFT_E_INVALID);
+  {
+    // SIFT_FLAG_FAST: the wave-pair pyramid (literal taps, checked against the
+    // host's) unless SIFT_HIP_FAST_V1=1 selects round 2's pyr_fast_kernel
+    const char* e = getenv("SIFT_HIP_FAST_V1");
+    c->fast_pair = pair_taps_match(c->fast_taps.data()) && !(e && atoi(e) != 0);
+  }
   MathConsts mc;
   host_math_consts(&mc);
   if (dmalloc(&c->d_coef, coefs.size()) != hipSuccess || dmalloc(&c->d_mc, 1) != hipSuccess ||

@@ -233,6 +233,12 @@ void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int n
                    float2* part_d, int2* part_i, int* idx, float* dist);
 void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
                          const void* coef);
+// pyramid_pair.hip (SIFT_FLAG_FAST, round 3): octave o's five planes; octave
+// o+1's plane 0 too when pyramid_pair_fuses(L, o + 1) (else decimate first).
+// pair_taps_match(FastCoefs block): the compile-time taps equal the host's.
+void launch_pyramid_pair(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
+bool pyramid_pair_fuses(const Layout& L, int o);
+bool pair_taps_match(const void* coef);
 
 // detect.hip
 struct DetectBufs {

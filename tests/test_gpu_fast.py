@@ -33,11 +33,29 @@ def fctx(siftgpu):
     c.close()
 
 
+@pytest.fixture(scope="module", params=["pair", "v1"])
+def fctx_both(request, siftgpu):
+    """Both SIFT_FLAG_FAST pyramids: pyramid_pair.hip (default, round 3) and
+    round 2's pyramid_fast.hip (SIFT_HIP_FAST_V1=1, read at context creation)."""
+    import os
+    old = os.environ.pop("SIFT_HIP_FAST_V1", None)
+    if request.param == "v1":
+        os.environ["SIFT_HIP_FAST_V1"] = "1"
+    try:
+        c = siftgpu.Context(1080, 1920, 4, device=0, flags=FAST)
+    finally:
+        os.environ.pop("SIFT_HIP_FAST_V1", None)
+        if old is not None:
+            os.environ["SIFT_HIP_FAST_V1"] = old
+    yield c
+    c.close()
+
+
 @pytest.mark.parametrize("shape,b", [((1080, 1920), 0), ((203, 157), 2), ((33, 1200), 12),
                                      ((300, 210), 3), ((130, 90), 6)])
-def test_fast_pyramid_close_to_exact(fctx, oracle, shape, b):
+def test_fast_pyramid_close_to_exact(fctx_both, oracle, shape, b):
     img = oracle.synth_image(b, *shape)
-    gp = fctx.buildGaussianPyramid(img, 5)
+    gp = fctx_both.buildGaussianPyramid(img, 5)
     ref = oracle.split_planes(oracle.build_gaussian_pyramid(img), *shape, 5, 5)
     errs = [float(np.abs(p.astype(np.float64) - q).max()) for p, q in zip(gp, ref)]
     assert max(errs) < PLANE_ATOL, errs
@@ -45,12 +63,12 @@ def test_fast_pyramid_close_to_exact(fctx, oracle, shape, b):
     assert errs[0] < 5e-4, errs[0]
 
 
-def test_fast_pyramid_border_rule(fctx):
+def test_fast_pyramid_border_rule(fctx_both):
     """The last source row and column never contribute (getSubMatrix, src/sift.cpp:116)."""
     img = np.zeros((64, 80), np.float32)
     img[-1, :] = 255
     img[:, -1] = 255
-    gp = fctx.buildGaussianPyramid(img, 3)
+    gp = fctx_both.buildGaussianPyramid(img, 3)
     for i, p in enumerate(gp):
         assert not p.any(), f"plane {i}"
 
