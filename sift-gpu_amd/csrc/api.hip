@@ -134,6 +134,9 @@ struct sift_ctx {
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
   std::vector<char> fast_taps;    // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip), passed by value
   bool fast_pair = true;          // SIFT_FLAG_FAST via pyramid_pair.hip (round 3)
+  // exact blur: launches with fewer 8-pixel tile workgroups than this use the
+  // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
+  long long small_max = 2048;
   size_t coef_gen_cap = 0;
   int wsz[4] = {0, 0, 0, 0};
   int w_base = 0;
@@ -364,6 +367,8 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       StageScope s(c, sym ? ST_BLUR_SYM : ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
       if (sym)
         launch_blur_octave_sym(st, L, o, c->d_gpyr, batch);
+      else if (blur_octave_tiles(L, o, batch) < c->small_max)
+        launch_blur_octave_small(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch);
       else
         launch_blur_octave(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch);
     }
@@ -678,6 +683,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     if (m) c->sym_min = atoi(m);
     const char* r = getenv("SIFT_HIP_SYM_ROWS_MIN");
     if (r) c->sym_rows = atoi(r);
+    const char* sm = getenv("SIFT_HIP_SMALL_MAX");
+    if (sm) c->small_max = atoll(sm);
   }
   c->fast_taps.resize(fast_coefs_size());
   if (fast_coefs_host(sb, sig_f, c->fast_taps.data()) != 0) return bail(SIFT_E_INVALID);

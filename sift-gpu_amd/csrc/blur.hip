@@ -252,6 +252,130 @@ void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, con
   hipLaunchKernelGGL(blur_octave_kernel, grid, dim3(256), lds_bytes_for(18), st, A);
 }
 
+// ---- exact 2-D blur, small launches (round 3) ---------------------------------
+// One 1080p image's octaves 1-3 give the 8-pixel-per-lane tiles only 80-1020
+// workgroups: a wave then sits alone on its SIMD and issues 8 x 2 x (2w+1)^2
+// instructions at one per 4 cycles (octaves 1-3: 81 / 63 / 65 us per launch,
+// round 2's single-image trace).  Here a lane owns 2 adjacent outputs of a
+// 32 x 16 tile, so a launch has 4x the waves and each wave a quarter of the
+// chain.  Same float chain per output as blur_tile (kernel rows ascending,
+// columns ascending, acc = acc + x * K, one / 8192 at the end), so the planes
+// are bit-identical.  The (2w+1)^2 table sits in LDS and each kernel row's
+// coefficients are read as broadcast ds_read_b128 into VGPRs (a VGPR operand
+// issues at full rate, an SGPR one at half); the window is 19 ds_read_b64 per
+// row for w = 18 (row pitch 96 = 32 mod 64 words: the two tile rows of a
+// 32-lane pass fill opposite bank halves, conflict free).
+constexpr int kSW = 32, kSH = 16, kSLP = 96;
+
+template <int W>
+struct SmallTile {
+  static constexpr int KS = 2 * W + 1;
+  static constexpr int KP = (KS + 3) / 4 * 4;  // coefficient row pitch (b128 reads)
+  static constexpr int LR = kSH + 2 * W, LW = kSW + 2 * W;
+  static constexpr int LDS_FLOATS = LR * kSLP + KS * KP;
+  static_assert(LW <= kSLP, "row pitch");
+};
+
+template <int W>
+__device__ __forceinline__ void blur_small_tile(const float* __restrict__ src, long long spitch, int rows, int cols,
+                                                float* __restrict__ dst, long long dpitch,
+                                                const float* __restrict__ coef, int x0, int y0,
+                                                float* __restrict__ lds) {
+  using T = SmallTile<W>;
+  const int t = threadIdx.x;
+  float* kt = lds + T::LR * kSLP;
+  for (int i = t; i < T::KS * T::KS; i += 256) {
+    const int a = i / T::KS, b = i - a * T::KS;
+    kt[a * T::KP + b] = coef[i];
+  }
+  for (int i = t; i < T::LR * T::LW; i += 256) {
+    const int r = i / T::LW, c = i - r * T::LW;
+    const int gy = y0 - W + r, gx = x0 - W + c;
+    const bool ok = gy >= 0 && gy < rows - 1 && gx >= 0 && gx < cols - 1;
+    lds[r * kSLP + c] = ok ? src[(long long)gy * spitch + gx] : 0.f;
+  }
+  __syncthreads();
+  const int tx = t & 15, ty = t >> 4;
+  float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll 1
+  for (int a = 0; a < T::KS; ++a) {
+    float k[T::KP];
+    const float4* k4 = reinterpret_cast<const float4*>(kt + a * T::KP);
+#pragma unroll
+    for (int q = 0; q < T::KP / 4; ++q) {
+      const float4 v = k4[q];
+      k[4 * q] = v.x;
+      k[4 * q + 1] = v.y;
+      k[4 * q + 2] = v.z;
+      k[4 * q + 3] = v.w;
+    }
+    float win[T::KS + 1];
+    const float2* w2 = reinterpret_cast<const float2*>(lds + (ty + a) * kSLP + 2 * tx);
+#pragma unroll
+    for (int q = 0; q < (T::KS + 1) / 2; ++q) {
+      const float2 v = w2[q];
+      win[2 * q] = v.x;
+      win[2 * q + 1] = v.y;
+    }
+#pragma unroll
+    for (int b = 0; b < T::KS; ++b) {
+      const float p0 = win[b] * k[b], p1 = win[b + 1] * k[b];
+      acc0 = acc0 + p0;
+      acc1 = acc1 + p1;
+    }
+  }
+  const int y = y0 + ty, x = x0 + 2 * tx;
+  if (y < rows) {
+    float* drow = dst + (long long)y * dpitch + x;
+    if (x < cols) drow[0] = acc0 / 8192.f;
+    if (x + 1 < cols) drow[1] = acc1 / 8192.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void blur_small_kernel(OctaveArgs A) {
+  extern __shared__ float4 lds4[];
+  float* lds = reinterpret_cast<float*>(lds4);
+  const int z = blockIdx.z;
+  const int b = z >> 2;
+  const int si = 3 - (z & 3);  // heaviest scale first
+  const float* src = A.gpyr + b * A.g_img + A.base_off;
+  float* dst = A.gpyr + b * A.g_img + A.dst_off[si];
+  const int x0 = blockIdx.x * kSW, y0 = blockIdx.y * kSH;
+  switch (si) {
+    case 0: blur_small_tile<4>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[0], x0, y0, lds); break;
+    case 1: blur_small_tile<8>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[1], x0, y0, lds); break;
+    case 2: blur_small_tile<12>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[2], x0, y0, lds); break;
+    default: blur_small_tile<18>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[3], x0, y0, lds); break;
+  }
+}
+
+// Workgroups of launch_blur_octave (8-pixel tiles) for this octave and batch.
+long long blur_octave_tiles(const Layout& L, int o, int batch) {
+  const Octave& O = L.oct[o];
+  return (long long)((O.cols + kTileW - 1) / kTileW) * ((O.rows + kTY - 1) / kTY) * batch * 4;
+}
+
+void launch_blur_octave_small(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
+                              const int* wsz, int batch) {
+  const Octave& O = L.oct[o];
+  OctaveArgs A;
+  A.gpyr = gpyr;
+  A.g_img = L.g_img;
+  A.base_off = O.g_off[0];
+  size_t coff = 0;
+  for (int s = 0; s < 4; ++s) {
+    A.dst_off[s] = O.g_off[s + 1];
+    A.coef[s] = coefs + coff;
+    coff += (size_t)(2 * wsz[s] + 1) * (2 * wsz[s] + 1);
+  }
+  A.pitch = O.pitch;
+  A.rows = O.rows;
+  A.cols = O.cols;
+  A.pad_ = 0;
+  dim3 grid((O.cols + kSW - 1) / kSW, (O.rows + kSH - 1) / kSH, batch * 4);
+  hipLaunchKernelGGL(blur_small_kernel, grid, dim3(256), SmallTile<18>::LDS_FLOATS * 4, st, A);
+}
+
 // ---- exact 2-D blur, symmetric scatter form (the SIFT_NCL tables) ----------
 // Same float chain per output as blur_tile, about 24 % fewer VALU instructions.
 // K[a][b] depends on a^2 + b^2 only (src/sift.cpp:103), so the product

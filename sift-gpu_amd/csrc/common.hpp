@@ -203,6 +203,11 @@ void launch_blur_plane(hipStream_t st, int w, const float* coef, Plane src, floa
                        long long dpitch, long long dimg, int rows, int cols, int batch);
 void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
                         const int* wsz, int batch);
+// The same planes for small launches (2 outputs per lane, 32 x 16 tiles;
+// round 3): picked when blur_octave_tiles(...) is below the context's limit.
+void launch_blur_octave_small(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
+                              const int* wsz, int batch);
+long long blur_octave_tiles(const Layout& L, int o, int batch);
 // Exact blur in symmetric scatter form for SIFT_NCL's five fixed tables
 // (compile-time constants); sym_tables_match(coefs) checks them against the
 // context's base + octave tables before these are used.
