@@ -106,9 +106,14 @@ struct RecT<true> {
 // DET: the keypoints come from this library's detection, so every window has
 // radius <= 40 (scl < 1.6 * 2^1.25, src/sift.cpp:588) and a row table: the
 // whole-window walk and its interior tests compile away.
-template <bool PACKED, bool DET>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 : 1))) void descriptor_kernel(
-    DescArgs A) {
+// PF: sample batches in flight.  1: the next batch's gather is issued and
+// used in the step that runs this batch's chain (default: with many waves per
+// SIMD the gather latency hides behind other waves).  2 (launches of one
+// image, round 3): its gather is issued a step earlier, so a wave that is
+// alone on its SIMD does not wait a full memory latency per batch.
+template <bool PACKED, bool DET, int PF = 1>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF == 2 ? 2 : PACKED ? 4 : 1))) void
+descriptor_kernel(DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
   // per-sample hand-off records (see RecT)
   __shared__ __attribute__((aligned(16))) float rec[PACKED ? kGrp * kRecG : 8 * kRecStride2];
@@ -266,22 +271,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
     // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
     // the owner adds its lane to form the [qidx][lane] address.
     RecT<PACKED> rc_cur;  // (qidx, val) x 8 corners of this lane's sample
-    auto sample = [&](bool in_range, RecT<PACKED>& out, int& odd_out) {
+    // locate: the sample at the walk position, its bins and its gather (in
+    // flight until finish uses it); finish: the weights and corner records.
+    struct Loc {
+      float c_rot, r_rot, rbin, cbin;
+      float2 mo_raw;
+      bool ok;
+    };
+    auto locate = [&](bool in_range, Loc& L) {
       const int i = ri - radius, j = rlo + u;
-      const float c_rot = j * cos_t - i * sin_t;
-      const float r_rot = j * sin_t + i * cos_t;
-      float rbin = r_rot + d / 2 - 0.5f;
-      float cbin = c_rot + d / 2 - 0.5f;
+      L.c_rot = j * cos_t - i * sin_t;
+      L.r_rot = j * sin_t + i * cos_t;
+      L.rbin = L.r_rot + d / 2 - 0.5f;
+      L.cbin = L.c_rot + d / 2 - 0.5f;
       const int r = py + i, c = px + j;
       // the row table enumerates interior pixels only (src/sift.cpp:620-621's
       // 0 < r < rows-1, 0 < c < cols-1), so only the whole-window walk tests them
-      const bool ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d &&
-                      (table || (r > 0 && r < rows - 1 && c > 0 && c < cols - 1));
+      L.ok = in_range && L.rbin > -1 && L.rbin < d && L.cbin > -1 && L.cbin < d &&
+             (table || (r > 0 && r < rows - 1 && c > 0 && c < cols - 1));
       // an invalid sample gathers from the clamped keypoint centre (any valid
       // address: its value is replaced below); plane offsets fit 32 bits
-      const float2 mo_raw = gimg[(unsigned)(ok ? r * pitch32 + c : ctr_off)];  // (Mag, Ori) of the pixel
+      L.mo_raw = gimg[(unsigned)(L.ok ? r * pitch32 + c : ctr_off)];  // (Mag, Ori) of the pixel
+    };
+    auto finish = [&](const Loc& L, RecT<PACKED>& out, int& odd_out) {
+      const float c_rot = L.c_rot, r_rot = L.r_rot;
+      float rbin = L.rbin, cbin = L.cbin;
+      const bool ok = L.ok;
       // invalid: (0, 0) -- border gradients are never written and may hold NaN
-      const float2 mo = ok ? mo_raw : make_float2(0.f, 0.f);
+      const float2 mo = ok ? L.mo_raw : make_float2(0.f, 0.f);
       const float w = exp32f_v<false>((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
       float obin = (mo.y - ori) * bins_per_rad;
       const float mag = mo.x * w;
@@ -333,6 +350,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
       }
       odd_out = odd;
     };
+    auto sample = [&](bool in_range, RecT<PACKED>& out, int& odd_out) {
+      Loc L;
+      locate(in_range, L);
+      finish(L, out, odd_out);
+    };
     // Entry ri+1 of the row table rides in a register (loaded one advance
     // ahead), so the common advance -- at most one row change -- is
     // branch-free selects with no LDS round trip; short or empty rows fall
@@ -360,9 +382,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
       enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
     };
     int odd_cur = 0;
+    Loc loc_nxt;  // PF = 2: batch k + 1, located and gathering
     if (nmax > 0) {
-      sample(q < nsamp, rc_cur, odd_cur);
-      advance();
+      if constexpr (PF == 2) {
+        Loc l0;
+        locate(q < nsamp, l0);
+        advance();
+        locate(8 + q < nsamp, loc_nxt);
+        advance();
+        finish(l0, rc_cur, odd_cur);
+      } else {
+        sample(q < nsamp, rc_cur, odd_cur);
+        advance();
+      }
     }
     for (int base = 0; base < nmax; base += 8) {
       if constexpr (PACKED) {
@@ -394,7 +426,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
       wave_sync_d();
       RecT<PACKED> rc_nxt;
       int odd_nxt = 0;
-      sample(base + 8 + q < nsamp, rc_nxt, odd_nxt);
+      Loc loc_2;
+      if constexpr (PF == 2) {
+        locate(base + 16 + q < nsamp, loc_2);  // batch k + 2: its gather flies for a whole step
+        advance();
+        finish(loc_nxt, rc_nxt, odd_nxt);
+      } else {
+        sample(base + 8 + q < nsamp, rc_nxt, odd_nxt);
+      }
       // ordered accumulation of batch k: lane q applies its record of each sample
       if constexpr (PACKED) {
         const char* rb = reinterpret_cast<const char*>(rec);
@@ -423,7 +462,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PACKED ? 4 :
         }
       }
       wave_sync_d();
-      advance();
+      if constexpr (PF == 2)
+        loc_nxt = loc_2;
+      else
+        advance();
       rc_cur = rc_nxt;
       odd_cur = odd_nxt;
     }
@@ -536,7 +578,18 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
     const char* e = getenv("SIFT_HIP_DESC_PACKED");  // A/B switch between the two record forms
     return !e || atoi(e) != 0;
   }();
-  if (packed && detected)
+  // one image per call (the single-image path): few waves, latency-bound
+  // chains -- gathers two batches ahead (SIFT_HIP_DESC_DEEP=0/1 overrides)
+  static const int deep_env = [] {
+    const char* e = getenv("SIFT_HIP_DESC_DEEP");
+    return e ? atoi(e) : -1;
+  }();
+  const bool deep = deep_env >= 0 ? deep_env != 0 : batch == 1;
+  if (packed && detected && deep)
+    hipLaunchKernelGGL((descriptor_kernel<true, true, 2>),
+                       dim3(resident_grid((const void*)descriptor_kernel<true, true, 2>, 64, 0, 8192)), dim3(64), 0, st,
+                       A);
+  else if (packed && detected)
     hipLaunchKernelGGL((descriptor_kernel<true, true>),
                        dim3(resident_grid((const void*)descriptor_kernel<true, true>, 64, 0, 8192)), dim3(64), 0, st, A);
   else if (packed)
