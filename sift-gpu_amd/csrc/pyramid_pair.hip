@@ -40,9 +40,10 @@
 //     step phases and picked by a uniform switch.
 //   planes leave through buffer stores whose offset is pushed past the plane
 //     for rows / columns outside the output range (no branches);
-//   plane 3 (w = 12) also writes the next octave's plane 0, its INTER_NEAREST
-//     half (src/sift.cpp:252-254) = (2y, 2x) when the next octave has exactly
-//     half the rows and columns (the caller decimates otherwise).
+//   plane 2 (w = 8; gpyr[(o-1)*nScales + nOctaveLayers], nOctaveLayers = 2)
+//     also writes the next octave's plane 0, its INTER_NEAREST half
+//     (src/sift.cpp:252-254) = (2y, 2x) when the next octave has exactly half
+//     the rows and columns (the caller decimates otherwise).
 //   the next step's source rows are loaded with instructions the compiler does
 //   not track and waited for with an explicit vmcnt that leaves this step's
 //   plane stores in flight (pp_ld, PP_WAIT).
@@ -178,6 +179,8 @@ struct PPOut {
   bool colok, xeven;
 };
 
+static_assert(kLayers == 2 && PScale<8>::plane == kLayers, "the decimated plane is wave B's w = 8 scale");
+
 // Source row J of a step at cycle phase M, both scales; oa / ob get the two
 // outputs it completes (rows Ys + J - WA and Ys + J - WB).
 template <int WA, int WB, int M, int J>
@@ -225,7 +228,7 @@ __device__ __forceinline__ void pp_dispatch(int m, float (&aa)[PScale<WA>::P], f
 }
 
 // The step's completed outputs (after the phase switch, so every path issues
-// the same stores), and plane 3's decimated copy for the next octave.
+// the same stores), and plane 2's decimated copy for the next octave.
 template <int WA, int WB>
 __device__ __forceinline__ void pp_stores(const float (&oa)[kPB], const float (&ob)[kPB], const PPOut& o) {
 #pragma unroll
@@ -233,9 +236,12 @@ __device__ __forceinline__ void pp_stores(const float (&oa)[kPB], const float (&
     const int ya = o.Ys + j - WA, yb = o.Ys + j - WB;
     pp_store(o.ra, (o.colok && ya >= o.y0 && ya < o.y1) ? (ya * o.pitch + o.x) * 4 : kDropP, oa[j]);
     pp_store(o.rb, (o.colok && yb >= o.y0 && yb < o.y1) ? (yb * o.pitch + o.x) * 4 : kDropP, ob[j]);
-    if constexpr (WA == 12) {  // plane 3 -> next octave's plane 0 at (ya / 2, x / 2)
-      const bool dn = o.xeven && (ya & 1) == 0 && ya >= o.y0 && ya < o.y1;
-      pp_store(o.rn, dn ? ((ya >> 1) * o.n_pitch + (o.x >> 1)) * 4 : kDropP, oa[j]);
+    // plane nOctaveLayers (= 2, src/sift.cpp:252) -> next octave's plane 0 at (y / 2, x / 2)
+    if constexpr (PScale<WA>::plane == kLayers || PScale<WB>::plane == kLayers) {
+      constexpr bool A_ = PScale<WA>::plane == kLayers;
+      const int yd = A_ ? ya : yb;
+      const bool dn = o.xeven && (yd & 1) == 0 && yd >= o.y0 && yd < o.y1;
+      pp_store(o.rn, dn ? ((yd >> 1) * o.n_pitch + (o.x >> 1)) * 4 : kDropP, A_ ? oa[j] : ob[j]);
     }
   }
 }
@@ -266,7 +272,8 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
   constexpr int PA = PScale<WA>::P, PB = PScale<WB>::P;
   // VMEM stores per step after the prefetch: base column pass (4, octave 0),
   // 2 per row (+1 decimation store per row on wave B)
-  constexpr int kStores = (OCT0 ? 4 : 0) + kPB * (WA == 12 ? 3 : 2);
+  constexpr bool kDec = PScale<WA>::plane == kLayers || PScale<WB>::plane == kLayers;
+  constexpr int kStores = (OCT0 ? 4 : 0) + kPB * (kDec ? 3 : 2);
   const int t = threadIdx.x, lane = t & 63;
   float* const gimg = A.gpyr + b * A.g_img;
   const long long plane_bytes = (long long)A.rows * A.pitch * 4;
