@@ -89,10 +89,6 @@ __device__ __forceinline__ void slab(float a, float inv_a, float b, int& lo, int
 //     waves per SIMD fit instead of three.
 constexpr int kRecG = 64;  // PACKED value words per group (8 owners x 8 samples, XOR-swizzled, see the store)
 
-// Byte-address swizzle of owner slot s in the PACKED value records (see the
-// store in descriptor_kernel): XOR-linear in s.
-__device__ __forceinline__ constexpr int rec_tb(int s) { return (s << 8) ^ ((s & 1) << 7) ^ (((s >> 1) & 1) << 4); }
-
 template <bool PACKED>
 struct RecT {  // one lane's 8 corner records: (qidx, value) pairs
   float4 r[4];
@@ -398,21 +394,22 @@ descriptor_kernel(DescArgs A) {
     }
     for (int base = 0; base < nmax; base += 8) {
       if constexpr (PACKED) {
-        // corner k to owner slot s = k ^ odd: value at byte (32g + 4q) ^ TB(s),
-        // TB(s) = 256 s ^ 128 (s & 1) ^ 16 ((s >> 1) & 1) (rec_tb).  The 32
-        // lanes of a ds_write_b32 pass (groups g..g+3) then hit banks
-        // (8g + q) ^ 4 ((s >> 1) & 1) mod 32: at most 2-way whatever the
-        // lanes' slots (free on a b32 store), where the old [g][owner][sample]
-        // layout put 4 lanes on 4 banks chosen by their random slots.  The
-        // owner's two ds_read_b128 stay conflict free (see the read).  TB is
-        // XOR-linear in s, so store k's address is one XOR of the per-batch
-        // base with the constant TB(k).  Bin byte at (g << 6) | (s << 3) | q.
+        // corner k to owner slot s = k ^ odd: value at byte (g << 8) | (s << 5) |
+        // (q << 2), bit 4 flipped on odd groups (so a 16-lane pass of the
+        // owners' ds_read_b128 -- an even and an odd group -- covers all 64
+        // banks); bin byte at (g << 6) | (s << 3) | q.  Slot bits are clear
+        // in both bases, so each address is one XOR with k's slot bits.
+        // (Round 3 measured a layout whose stores are at most 2-way
+        // conflicted -- value at (32g + 4q) ^ TB(s), TB XOR-linear in s, reads
+        // still conflict free: SQ_LDS_BANK_CONFLICT -35 %, but the slot
+        // swizzle costs ~3 VALU per batch and the kernel took 7.57-7.69 vs
+        // 7.45-7.47 ms: it is bound by VALU issue, not by the conflicts.)
         char* rb = reinterpret_cast<char*>(rec);
-        const int wv = ((g << 5) | (q << 2)) ^ rec_tb(odd_cur);
+        const int wv = ((g << 8) | ((q << 2) ^ ((g & 1) << 4))) | (odd_cur << 5);
         const int wq = ((g << 6) | q) | (odd_cur << 3);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          *reinterpret_cast<float*>(rb + (wv ^ rec_tb(k))) = rc_cur.v[k];
+          *reinterpret_cast<float*>(rb + (wv ^ (k << 5))) = rc_cur.v[k];
           recq[wq ^ (k << 3)] = (unsigned char)(rc_cur.qb[k >> 2] >> (8 * (k & 3)));
         }
       } else {
@@ -437,14 +434,9 @@ descriptor_kernel(DescArgs A) {
       // ordered accumulation of batch k: lane q applies its record of each sample
       if constexpr (PACKED) {
         const char* rb = reinterpret_cast<const char*>(rec);
-        // owner q's 8 values, samples 0-3 then 4-7: bytes 256 q + ((32 g +
-        // 16 h) ^ 128 (q & 1)) and the other half (h = (q >> 1) & 1).  In each
-        // 16-lane pass of a ds_read_b128 (4 lanes of each of 4 groups) the
-        // 16-byte slots (2g + h) ^ 8 (q & 1) mod 16 are all distinct.
-        const int hq = (q >> 1) & 1;
-        const int rv = q << 8, rx = (q & 1) << 7;
-        const float4 va = *reinterpret_cast<const float4*>(rb + (rv | (((g << 5) | (hq << 4)) ^ rx)));
-        const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | (((g << 5) | ((hq ^ 1) << 4)) ^ rx)));
+        const int rv = (g << 8) | (q << 5);  // samples 0-3 at bit 4 = g & 1, samples 4-7 at the other half
+        const float4 va = *reinterpret_cast<const float4*>(rb + (rv | ((g & 1) << 4)));
+        const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | (((g & 1) ^ 1) << 4)));
         const uint2 qq = *reinterpret_cast<const uint2*>(recq + lane * 8);
         const float vals[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
 #pragma unroll

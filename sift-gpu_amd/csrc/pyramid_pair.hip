@@ -75,9 +75,14 @@ constexpr int kIPit = 112;      // image row pitch
 constexpr int kHbRows = 12;     // base row-pass ring: rows [Y - 4, Y + 8)
 constexpr int kHbPit = 100;
 constexpr int kDropP = 0x7ffffff0;  // buffer offset past every plane: the store is dropped
-constexpr int kImgPer = (kPB * kIC + 127) / 128;       // 4 image loads per thread per step
-constexpr int kSrcPer = (kPB * (kBC / 2) + 127) / 128;  // 2 float2 plane loads per thread per step
-static_assert(kImgPer == 4 && kSrcPer == 2, "PP_WAIT operand lists");
+constexpr int kImgPer = 4;  // image loads per wave per step: 2 rows x (64 + 44 columns)
+constexpr int kSrcPer = 2;  // float2 plane loads per wave per step: 2 rows x 50 pairs
+static_assert(kIC - 64 <= 64 && kBC / 2 <= 64, "a row in two loads / one float2 load");
+// Store offsets: voffset (per lane, fixed) + soffset (per row, wave-uniform).
+// Either part alone pushes the sum past every plane (planes stay below
+// kDropV bytes: launch_pyramid_pair's caller checks), and two drop parts
+// still fit 32 bits.
+constexpr unsigned kDropV = 0x7f000000u;
 
 struct PairLds0 {  // octave 0
   float base[2][kPB][kBPit];
@@ -99,18 +104,23 @@ __device__ __forceinline__ PRsrc pp_rsrc(float* p, long long bytes) {
 __device__ __forceinline__ void pp_store(PRsrc rs, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, off, 0, 0);
 }
+__device__ __forceinline__ void pp_store_s(PRsrc rs, unsigned voff, unsigned soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, (int)soff, 0);
+}
 
 // Untracked loads (see the file comment): the destination is written when the
 // explicit wait that names it as an operand returns.  The memory clobber keeps
 // later stores after them (the wait counts the stores that follow).
-__device__ __forceinline__ float pp_ld1(const float* p) {
+// saddr form: address = the 64-bit SGPR base (a wave-uniform row) + a 32-bit
+// per-lane byte offset.
+__device__ __forceinline__ float pp_lds1(unsigned voff, const float* sbase) {
   float v;
-  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase) : "memory");
   return v;
 }
-__device__ __forceinline__ pf2 pp_ld2(const float* p) {
+__device__ __forceinline__ pf2 pp_lds2(unsigned voff, const float* sbase) {
   pf2 v;
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase) : "memory");
   return v;
 }
 
@@ -175,8 +185,8 @@ __device__ __forceinline__ void pp_scatter(float (&acc)[PScale<W>::P], float h) 
 
 struct PPOut {
   PRsrc ra, rb, rn;
-  int Ys, y0, y1, x, pitch, n_pitch;
-  bool colok, xeven;
+  int Ys, y0, y1, pitch4, n_pitch4;
+  unsigned vx, vxn;  // per-lane voffsets: plane column, decimated column (or kDropV)
 };
 
 static_assert(kLayers == 2 && PScale<8>::plane == kLayers, "the decimated plane is wave B's w = 8 scale");
@@ -233,20 +243,19 @@ template <int WA, int WB>
 __device__ __forceinline__ void pp_stores(const float (&oa)[kPB], const float (&ob)[kPB], const PPOut& o) {
 #pragma unroll
   for (int j = 0; j < kPB; ++j) {
-    const int ya = o.Ys + j - WA, yb = o.Ys + j - WB;
-    pp_store(o.ra, (o.colok && ya >= o.y0 && ya < o.y1) ? (ya * o.pitch + o.x) * 4 : kDropP, oa[j]);
-    pp_store(o.rb, (o.colok && yb >= o.y0 && yb < o.y1) ? (yb * o.pitch + o.x) * 4 : kDropP, ob[j]);
+    const int ya = o.Ys + j - WA, yb = o.Ys + j - WB;  // wave-uniform rows: scalar offsets
+    pp_store_s(o.ra, o.vx, (ya >= o.y0 && ya < o.y1) ? (unsigned)(ya * o.pitch4) : kDropV, oa[j]);
+    pp_store_s(o.rb, o.vx, (yb >= o.y0 && yb < o.y1) ? (unsigned)(yb * o.pitch4) : kDropV, ob[j]);
     // plane nOctaveLayers (= 2, src/sift.cpp:252) -> next octave's plane 0 at (y / 2, x / 2)
     if constexpr (PScale<WA>::plane == kLayers || PScale<WB>::plane == kLayers) {
       constexpr bool A_ = PScale<WA>::plane == kLayers;
       const int yd = A_ ? ya : yb;
-      const bool dn = o.xeven && (yd & 1) == 0 && yd >= o.y0 && yd < o.y1;
-      pp_store(o.rn, dn ? ((yd >> 1) * o.n_pitch + (o.x >> 1)) * 4 : kDropP, A_ ? oa[j] : ob[j]);
+      const bool dn = (yd & 1) == 0 && yd >= o.y0 && yd < o.y1;
+      pp_store_s(o.rn, o.vxn, dn ? (unsigned)((yd >> 1) * o.n_pitch4) : kDropV, A_ ? oa[j] : ob[j]);
     }
   }
 }
 
-// N dropped stores (keeps the VMEM count after a prefetch fixed).
 // Distinct, non-adjacent offsets: identical stores to one address would be
 // merged, adjacent ones combined into one wide store.
 template <int N>
@@ -285,11 +294,13 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
   const PRsrc r0 = pp_rsrc(gimg + A.off[0], plane_bytes);
   o.y0 = y0;
   o.y1 = y1;
-  o.x = x0 + lane;
-  o.pitch = A.pitch;
-  o.n_pitch = A.n_pitch;
-  o.colok = o.x < A.cols;
-  o.xeven = (o.x & 1) == 0 && o.x < A.cols;
+  o.pitch4 = A.pitch * 4;
+  o.n_pitch4 = A.n_pitch * 4;
+  {
+    const int x = x0 + lane;
+    o.vx = x < A.cols ? (unsigned)x * 4u : kDropV;
+    o.vxn = ((x & 1) == 0 && x < A.cols) ? (unsigned)(x >> 1) * 4u : kDropV;
+  }
   const float* src = A.src + b * A.s_img;
   const int rows = A.rows, cols = A.cols;
   const int Ystart = y0 - kLead;
@@ -300,64 +311,70 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
 #pragma unroll
   for (int k = 0; k < PB; ++k) ab[k] = 0.f;
 
-  // per-thread staging geometry (loop invariant)
-  int ij[kImgPer], ic[kImgPer];   // octave 0: image element t + 128k -> (row, column)
-  int sj[kSrcPer], sc[kSrcPer];   // octave > 0: float2 element t + 128k -> (row, column pair)
+  // Source staging: wave wv loads rows 2wv, 2wv + 1 of the step's four, whole
+  // rows across its lanes, with the row base in SGPRs (global_load saddr form)
+  // and a per-lane column offset fixed for the walk -- no per-step address
+  // VALU.  Columns are clamped into the row (any valid address; padding is
+  // applied when the values are staged).
+  //   octave 0: image columns [x0 - 22, x0 + 86): lanes 0..63 and 0..43
+  //   octave > 0: plane-0 columns [x0 - 18, x0 + 82) as float2, lanes 0..49
+  unsigned voff[2];
+  bool cval[2];
+  if constexpr (OCT0) {
 #pragma unroll
-  for (int k = 0; k < kImgPer; ++k) {
-    const int e = t + 128 * k;
-    ij[k] = e / kIC;
-    ic[k] = e - ij[k] * kIC;
-  }
-#pragma unroll
-  for (int k = 0; k < kSrcPer; ++k) {
-    const int e = t + 128 * k;
-    sj[k] = e / (kBC / 2);
-    sc[k] = 2 * (e - sj[k] * (kBC / 2));
+    for (int h = 0; h < 2; ++h) {
+      const int c = x0 - 22 + lane + 64 * h;
+      voff[h] = (unsigned)min(max(c, 0), cols - 1) * 4u;
+      cval[h] = lane + 64 * h < kIC && c >= 0 && c < cols - 1;
+    }
+  } else {
+    const int c = x0 - kPH + 2 * min(lane, kBC / 2 - 1);
+    voff[0] = (unsigned)min(max(c, 0), A.pitch - 2) * 4u;
+    voff[1] = 0;
+    cval[0] = c >= 0 && c < cols - 1;
+    cval[1] = c + 1 >= 0 && c + 1 < cols - 1;
   }
   float pi[kImgPer];
   pf2 ps[kSrcPer];
+  const int rw = 2 * wv;  // this wave's first row of the four
+  auto row_base = [&](int r) {
+    return src + (long long)min(max(r, 0), rows - 1) * A.s_pitch;
+  };
   // rows [r0, r0 + 4) of the step's source into the prefetch registers
   auto fetch = [&](int r0) {
     if constexpr (OCT0) {
 #pragma unroll
-      for (int k = 0; k < kImgPer; ++k) {
-        const int r = min(max(r0 + ij[k], 0), rows - 1);
-        const int c = min(max(x0 - 22 + ic[k], 0), cols - 1);
-        pi[k] = pp_ld1(src + (long long)r * A.s_pitch + c);
+      for (int i = 0; i < 2; ++i) {
+        const float* rb = row_base(r0 + rw + i);
+        pi[2 * i] = pp_lds1(voff[0], rb);
+        pi[2 * i + 1] = pp_lds1(voff[1], rb);
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < kSrcPer; ++k) {
-        const int r = min(max(r0 + sj[k], 0), rows - 1);
-        const int c = min(max(x0 - kPH + sc[k], 0), A.pitch - 2);
-        ps[k] = pp_ld2(src + (long long)r * A.s_pitch + c);
-      }
+      for (int i = 0; i < 2; ++i) ps[i] = pp_lds2(voff[0], row_base(r0 + rw + i));
     }
   };
   // octave 0: image rows [r0, r0 + 4) with the base blur's source padding
   auto stage_img = [&](PairLds0& L, int r0) {
 #pragma unroll
-    for (int k = 0; k < kImgPer; ++k) {
-      const int e = t + 128 * k;
-      if (e < kPB * kIC) {
-        const int r = r0 + ij[k], c = x0 - 22 + ic[k];
-        L.img[ij[k]][ic[k]] = (r >= 0 && r < rows - 1 && c >= 0 && c < cols - 1) ? pi[k] : 0.f;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int r = r0 + rw + i;
+      const bool rok = r >= 0 && r < rows - 1;
+      L.img[rw + i][lane] = (rok && cval[0]) ? pi[2 * i] : 0.f;
+      if (lane < kIC - 64) L.img[rw + i][lane + 64] = (rok && cval[1]) ? pi[2 * i + 1] : 0.f;
     }
   };
   // octave > 0: plane-0 rows [r0, r0 + 4) -> padded base rows
   auto stage_src = [&](PairLdsN& L, int buf, int r0) {
 #pragma unroll
-    for (int k = 0; k < kSrcPer; ++k) {
-      const int e = t + 128 * k;
-      if (e < kPB * (kBC / 2)) {
-        const int r = r0 + sj[k], c = x0 - kPH + sc[k];
-        const bool rok = r >= 0 && r < rows - 1;
+    for (int i = 0; i < 2; ++i) {
+      const int r = r0 + rw + i;
+      const bool rok = r >= 0 && r < rows - 1;
+      if (lane < kBC / 2) {
         pf2 v;
-        v.x = (rok && c >= 0 && c < cols - 1) ? ps[k].x : 0.f;
-        v.y = (rok && c + 1 >= 0 && c + 1 < cols - 1) ? ps[k].y : 0.f;
-        *reinterpret_cast<pf2*>(&L.base[buf][sj[k]][sc[k]]) = v;
+        v.x = (rok && cval[0]) ? ps[i].x : 0.f;
+        v.y = (rok && cval[1]) ? ps[i].y : 0.f;
+        *reinterpret_cast<pf2*>(&L.base[buf][rw + i][2 * lane]) = v;
       }
     }
   };
@@ -427,7 +444,7 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
           hv[q] = L.hb[sl >= kHbRows ? sl - kHbRows : sl][tc];
         }
         const int xb = x0 - kPH + t;
-        const bool cout = t >= kPH && t < kPH + kPW && xb < cols;
+        const unsigned v0 = (t >= kPH && t < kPH + kPW && xb < cols) ? (unsigned)xb * 4u : kDropV;
         const bool cpad = t < kBC && xb >= 0 && xb < cols - 1;
 #pragma unroll
         for (int j = 0; j < kPB; ++j) {
@@ -435,7 +452,7 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
 #pragma unroll
           for (int k = 1; k <= 4; ++k) v = fmaf(kFastT0[k], hv[4 + j - k] + hv[4 + j + k], v);
           const int y = Ys + j;
-          pp_store(r0, (cout && y >= y0 && y < y1) ? (y * A.pitch + xb) * 4 : kDropP, v);
+          pp_store_s(r0, v0, (y >= y0 && y < y1) ? (unsigned)(y * A.pitch * 4) : kDropV, v);
           L.base[buf][j][t] = (cpad && y >= 0 && y < rows - 1) ? v : 0.f;
         }
       }

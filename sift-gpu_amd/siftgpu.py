@@ -108,7 +108,10 @@ def lib():
             "sift_bgr8_to_gray_device": (ip, [vp, vp, ip, ip, ip, sz, sz, ip, ip, vp, sz, sz]),
             "sift_knn_match_l1_device": (ip, [vp, vp, ip, vp, ip, ip, vp, vp]),
         }
+        optional = {"sift_graph_stats"}  # absent from older builds (A/B runs against a saved library)
         for name, (res, args) in sigs.items():
+            if name in optional and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
