@@ -416,13 +416,17 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
           v[4 * q + 2] = f.z;
           v[4 * q + 3] = f.w;
         }
-        float hv[4];
+        float hv[4];  // k outer, columns inner (see the scale row pass)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          float h = kFastT0[0] * v[4 + u];
+        for (int u = 0; u < 4; ++u) hv[u] = kFastT0[0] * v[4 + u];
 #pragma unroll
-          for (int k = 1; k <= 4; ++k) h = fmaf(kFastT0[k], v[4 + u - k] + v[4 + u + k], h);
-          hv[u] = h;
+        for (int k = 1; k <= 4; ++k) {
+          float pk[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) pk[u] = v[4 + u - k] + v[4 + u + k];
+          asm volatile("" : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]), "+v"(pk[3]));
+#pragma unroll
+          for (int u = 0; u < 4; ++u) hv[u] = fmaf(kFastT0[k], pk[u], hv[u]);
         }
         const int slot = (kPB * (s + 3) + j) % kHbRows;  // ring slot of row Ys + 4 + j (s >= -2)
         *reinterpret_cast<float4*>(&L.hb[slot][4 * i]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
@@ -446,11 +450,21 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
         const int xb = x0 - kPH + t;
         const unsigned v0 = (t >= kPH && t < kPH + kPW && xb < cols) ? (unsigned)xb * 4u : kDropV;
         const bool cpad = t < kBC && xb >= 0 && xb < cols - 1;
+        float bv[kPB];  // k outer, rows inner (see the scale row pass)
+#pragma unroll
+        for (int j = 0; j < kPB; ++j) bv[j] = kFastT0[0] * hv[4 + j];
+#pragma unroll
+        for (int k = 1; k <= 4; ++k) {
+          float pk[kPB];
+#pragma unroll
+          for (int j = 0; j < kPB; ++j) pk[j] = hv[4 + j - k] + hv[4 + j + k];
+          asm volatile("" : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]), "+v"(pk[3]));
+#pragma unroll
+          for (int j = 0; j < kPB; ++j) bv[j] = fmaf(kFastT0[k], pk[j], bv[j]);
+        }
 #pragma unroll
         for (int j = 0; j < kPB; ++j) {
-          float v = kFastT0[0] * hv[4 + j];
-#pragma unroll
-          for (int k = 1; k <= 4; ++k) v = fmaf(kFastT0[k], hv[4 + j - k] + hv[4 + j + k], v);
+          const float v = bv[j];
           const int y = Ys + j;
           pp_store_s(r0, v0, (y >= y0 && y < y1) ? (unsigned)(y * A.pitch * 4) : kDropV, v);
           L.base[buf][j][t] = (cpad && y >= 0 && y < rows - 1) ? v : 0.f;
@@ -486,19 +500,27 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
         v[4 * q + 2] = f.z;
         v[4 * q + 3] = f.w;
       }
+      // k outer, the 4 columns inner: the 4 pair sums of a tap, then the 8
+      // fma of the 8 chains -- every instruction's operands were produced >= 4
+      // instructions earlier (column-outer order made hipcc issue each fma
+      // right behind the add or fma it depends on: 0.44 of the VALU issue rate)
       float ha[4], hb[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float x = v[kPH + u];
-        float a = ptap<WA>(0) * x, c = ptap<WB>(0) * x;
+        ha[u] = ptap<WA>(0) * v[kPH + u];
+        hb[u] = ptap<WB>(0) * v[kPH + u];
+      }
 #pragma unroll
-        for (int k = 1; k <= WA; ++k) {
-          const float pk = v[kPH + u - k] + v[kPH + u + k];
-          a = fmaf(ptap<WA>(k), pk, a);
-          if (k <= WB) c = fmaf(ptap<WB>(k), pk, c);
+      for (int k = 1; k <= WA; ++k) {
+        float pk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pk[u] = v[kPH + u - k] + v[kPH + u + k];
+        asm volatile("" : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]), "+v"(pk[3]));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          ha[u] = fmaf(ptap<WA>(k), pk[u], ha[u]);
+          if (k <= WB) hb[u] = fmaf(ptap<WB>(k), pk[u], hb[u]);
         }
-        ha[u] = a;
-        hb[u] = c;
       }
       const int j = lane >> 4, i = lane & 15;
       *reinterpret_cast<float4*>(&hbuf[0][j][4 * i]) = make_float4(ha[0], ha[1], ha[2], ha[3]);
