@@ -57,6 +57,17 @@
 
 #include <utility>
 
+#ifndef PP_WPE
+#define PP_WPE 3
+#endif
+// Phase ablation (timing experiments only; results are garbage when set):
+// 1 = no row-pass window reads, 2 = no column-pass FMAs, 4 = every plane store
+// dropped, 8 = no workgroup barriers, 16 = no source loads, 32 = one column-pass
+// phase body instead of ten (code size).
+#ifndef PP_ABL
+#define PP_ABL 0
+#endif
+
 namespace sift {
 
 #include "../build/sym_coefs.inc"
@@ -71,32 +82,29 @@ constexpr int kLead = 20;       // rows walked above the chunk (>= kPH, multiple
 constexpr int kBC = kPW + 2 * kPH;   // 100 base columns per strip: [x0 - 18, x0 + 82)
 constexpr int kBPit = 128;      // base row pitch (floats): the row pass's b128 reads are conflict free
 constexpr int kIC = kBC + 8;    // 108 staged image columns: [x0 - 22, x0 + 86)
-constexpr int kIPit = 112;      // image row pitch
 constexpr int kHbRows = 12;     // base row-pass ring: rows [Y - 4, Y + 8)
 constexpr int kHbPit = 100;
 constexpr int kDropP = 0x7ffffff0;  // buffer offset past every plane: the store is dropped
-constexpr int kImgPer = 4;  // image loads per wave per step: 2 rows x (64 + 44 columns)
-constexpr int kSrcPer = 2;  // float2 plane loads per wave per step: 2 rows x 50 pairs
-static_assert(kIC - 64 <= 64 && kBC / 2 <= 64, "a row in two loads / one float2 load");
+static_assert(kIC <= 128 && kBC <= 128 && kBPit == 128, "a staged row is two 64-lane DMA loads");
 // Store offsets: voffset (per lane, fixed) + soffset (per row, wave-uniform).
 // Either part alone pushes the sum past every plane (planes stay below
 // kDropV bytes: launch_pyramid_pair's caller checks), and two drop parts
 // still fit 32 bits.
 constexpr unsigned kDropV = 0x7f000000u;
 
+constexpr int kRing = 3;  // source rows in flight: steps s, s + 1 landed / landing, s + 2 issued
 struct PairLds0 {  // octave 0
   float base[2][kPB][kBPit];
   float h[2][2][kPB][kPW];  // [wave][scale][row][column]
-  float img[kPB][kIPit];
+  float img[kRing][kPB][kBPit];  // image rows, LDS-DMA ring (columns [x0 - 22, x0 + 106))
   float hb[kHbRows][kHbPit];
 };
 struct PairLdsN {  // octave > 0
-  float base[2][kPB][kBPit];
+  float base[kRing][kPB][kBPit];  // plane-0 rows, LDS-DMA ring (columns [x0 - 18, x0 + 110))
   float h[2][2][kPB][kPW];
 };
 
 typedef __amdgpu_buffer_rsrc_t PRsrc;
-typedef float pf2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ PRsrc pp_rsrc(float* p, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)bytes, 0x00020000);
@@ -105,27 +113,29 @@ __device__ __forceinline__ void pp_store(PRsrc rs, int off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, off, 0, 0);
 }
 __device__ __forceinline__ void pp_store_s(PRsrc rs, unsigned voff, unsigned soff, float v) {
+  if constexpr (PP_ABL & 4) soff = kDropV;
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, (int)soff, 0);
 }
 
-// Untracked loads (see the file comment): the destination is written when the
-// explicit wait that names it as an operand returns.  The memory clobber keeps
-// later stores after them (the wait counts the stores that follow).
-// saddr form: address = the 64-bit SGPR base (a wave-uniform row) + a 32-bit
-// per-lane byte offset.
-__device__ __forceinline__ float pp_lds1(unsigned voff, const float* sbase) {
-  float v;
-  asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase) : "memory");
-  return v;
+// Source rows go straight to LDS (buffer_load_dword ... lds: lane l's dword
+// lands at M0 + 4l).  Out-of-range offsets read 0, which is how the padding
+// rows and columns (outside [0, rows-1) x [0, cols-1), getSubMatrix :116)
+// arrive as zeros with no select.  The wave waits for its own loads with an
+// explicit vmcnt and the workgroup barrier then covers the other wave's.
+__device__ __forceinline__ void pp_dma(unsigned lds_byte, unsigned voff, PRsrc rs, unsigned soff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, %3 offen lds"
+               ::"s"(lds_byte), "v"(voff), "s"(rs), "s"(soff) : "memory", "m0");
 }
-__device__ __forceinline__ pf2 pp_lds2(unsigned voff, const float* sbase) {
-  pf2 v;
-  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase) : "memory");
-  return v;
+__device__ __forceinline__ unsigned pp_lds_addr(const float* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(const __attribute__((address_space(3))) float*)p);
 }
 
 __device__ __forceinline__ void pp_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if constexpr (PP_ABL & 8)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 __device__ __forceinline__ void pp_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -172,6 +182,10 @@ namespace {
 template <int W, int R>
 __device__ __forceinline__ void pp_scatter(float (&acc)[PScale<W>::P], float h) {
   constexpr int P = PScale<W>::P;
+  if constexpr (PP_ABL & 2) {
+    acc[((R - W) % P + P) % P] = h;
+    return;
+  }
 #pragma unroll
   for (int d = -W; d <= W; ++d) {
     const int slot = ((R - d) % P + P) % P;
@@ -223,6 +237,10 @@ __device__ __forceinline__ void pp_dispatch(int m, float (&aa)[PScale<WA>::P], f
                                             const float (&ha)[kPB], const float (&hb)[kPB], float (&oa)[kPB],
                                             float (&ob)[kPB]) {
   static_assert(kPer == 10, "cases");
+  if constexpr ((PP_ABL & 32) != 0) {  // ablation: one phase body only (code size)
+    pp_step<WA, WB, 0>(aa, ab, ha, hb, oa, ob);
+    return;
+  }
   switch (m) {
     case 0: pp_step<WA, WB, 0>(aa, ab, ha, hb, oa, ob); break;
     case 1: pp_step<WA, WB, 1>(aa, ab, ha, hb, oa, ob); break;
@@ -264,15 +282,8 @@ __device__ __forceinline__ void pp_pad(PRsrc rs) {
   for (int i = 0; i < N; ++i) pp_store(rs, kDropP - 64 * i, 0.f);
 }
 
-// Wait for the step's source loads; N = VMEM stores issued after them.
-#define PP_WAIT(N, OCT0)                                                                                  \
-  do {                                                                                                    \
-    if constexpr (OCT0)                                                                                   \
-      asm volatile("s_waitcnt vmcnt(%4)" : "+v"(pi[0]), "+v"(pi[1]), "+v"(pi[2]), "+v"(pi[3]) : "n"(N)    \
-                   : "memory");                                                                           \
-    else                                                                                                  \
-      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(ps[0]), "+v"(ps[1]) : "n"(N) : "memory");                \
-  } while (0)
+// Wait for the step's source loads; N = VMEM operations issued after them.
+#define PP_WAIT(N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory")
 
 // One wave's walk over the workgroup's strip; wave A (WA, WB) = (18, 4),
 // wave B = (12, 8).  Both waves run the same barrier sequence.
@@ -311,102 +322,60 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
 #pragma unroll
   for (int k = 0; k < PB; ++k) ab[k] = 0.f;
 
-  // Source staging: wave wv loads rows 2wv, 2wv + 1 of the step's four, whole
-  // rows across its lanes, with the row base in SGPRs (global_load saddr form)
-  // and a per-lane column offset fixed for the walk -- no per-step address
-  // VALU.  Columns are clamped into the row (any valid address; padding is
-  // applied when the values are staged).
-  //   octave 0: image columns [x0 - 22, x0 + 86): lanes 0..63 and 0..43
-  //   octave > 0: plane-0 columns [x0 - 18, x0 + 82) as float2, lanes 0..49
+  // Source staging: wave wv loads rows 2wv, 2wv + 1 of a step's four, each as
+  // two 64-lane LDS-DMA loads (columns c0 + lane, c0 + 64 + lane; c0 = x0 - 22
+  // for the image, x0 - 18 for plane 0); per-lane column offsets are fixed for
+  // the walk, the row offset is a scalar; invalid positions are out of range
+  // and land as 0.
+  const int c0 = OCT0 ? x0 - 22 : x0 - kPH;
   unsigned voff[2];
-  bool cval[2];
-  if constexpr (OCT0) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = x0 - 22 + lane + 64 * h;
-      voff[h] = (unsigned)min(max(c, 0), cols - 1) * 4u;
-      cval[h] = lane + 64 * h < kIC && c >= 0 && c < cols - 1;
-    }
-  } else {
-    const int c = x0 - kPH + 2 * min(lane, kBC / 2 - 1);
-    voff[0] = (unsigned)min(max(c, 0), A.pitch - 2) * 4u;
-    voff[1] = 0;
-    cval[0] = c >= 0 && c < cols - 1;
-    cval[1] = c + 1 >= 0 && c + 1 < cols - 1;
+  for (int h = 0; h < 2; ++h) {
+    const int c = c0 + lane + 64 * h;
+    voff[h] = (c >= 0 && c < cols - 1) ? (unsigned)c * 4u : kDropV;
   }
-  float pi[kImgPer];
-  pf2 ps[kSrcPer];
+  const PRsrc rsrc = pp_rsrc(const_cast<float*>(src), (long long)rows * A.s_pitch * 4);
   const int rw = 2 * wv;  // this wave's first row of the four
-  auto row_base = [&](int r) {
-    return src + (long long)min(max(r, 0), rows - 1) * A.s_pitch;
-  };
-  // rows [r0, r0 + 4) of the step's source into the prefetch registers
-  auto fetch = [&](int r0) {
-    if constexpr (OCT0) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const float* rb = row_base(r0 + rw + i);
-        pi[2 * i] = pp_lds1(voff[0], rb);
-        pi[2 * i + 1] = pp_lds1(voff[1], rb);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) ps[i] = pp_lds2(voff[0], row_base(r0 + rw + i));
-    }
-  };
-  // octave 0: image rows [r0, r0 + 4) with the base blur's source padding
-  auto stage_img = [&](PairLds0& L, int r0) {
+  float* const ring = OCT0 ? &static_cast<PairLds0*>(ldsv)->img[0][0][0] : &static_cast<PairLdsN*>(ldsv)->base[0][0][0];
+  // rows [r0, r0 + 4) of a step into ring slot sl
+  auto issue = [&](int r0, int sl) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r = r0 + rw + i;
-      const bool rok = r >= 0 && r < rows - 1;
-      L.img[rw + i][lane] = (rok && cval[0]) ? pi[2 * i] : 0.f;
-      if (lane < kIC - 64) L.img[rw + i][lane + 64] = (rok && cval[1]) ? pi[2 * i + 1] : 0.f;
+      const unsigned soff = (r >= 0 && r < rows - 1) ? (unsigned)(r * A.s_pitch * 4) : kDropV;
+      float* dst = ring + (sl * kPB + rw + i) * kBPit;
+      pp_dma(pp_lds_addr(dst), voff[0], rsrc, soff);
+      pp_dma(pp_lds_addr(dst + 64), voff[1], rsrc, soff);
     }
   };
-  // octave > 0: plane-0 rows [r0, r0 + 4) -> padded base rows
-  auto stage_src = [&](PairLdsN& L, int buf, int r0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = r0 + rw + i;
-      const bool rok = r >= 0 && r < rows - 1;
-      if (lane < kBC / 2) {
-        pf2 v;
-        v.x = (rok && cval[0]) ? ps[i].x : 0.f;
-        v.y = (rok && cval[1]) ? ps[i].y : 0.f;
-        *reinterpret_cast<pf2*>(&L.base[buf][rw + i][2 * lane]) = v;
-      }
-    }
-  };
+  constexpr int kLoads = 4;                   // DMA loads per wave per step
+  constexpr int kWaitN = 2 * kStores + kLoads;  // VMEM operations after a step's loads at its wait
+  // source rows of step t: the image rows its base row pass needs (octave 0)
+  // or its base rows (octave > 0)
+  auto src_row = [&](int t) { return Ystart + kPB * t + (OCT0 ? kPB : 0); };
 
   const int s0 = OCT0 ? -2 : 0;
-  fetch(OCT0 ? Ystart + kPB * s0 + kPB : Ystart);
+  // steps s0 and s0 + 1 in flight, each followed by kStores dropped stores so
+  // every wait below sees exactly kWaitN younger operations
+  issue(src_row(s0), (s0 + kRing) % kRing);
+  pp_pad<kStores>(r0);
+  issue(src_row(s0 + 1), (s0 + 1 + kRing) % kRing);
   pp_pad<kStores>(r0);
   for (int s = s0; s < nsteps; ++s) {
     const int Ys = Ystart + kPB * s;
     const int buf = s & 1;
-    // ---- stage this step's source rows, prefetch the next step's ----
-    // Exactly kStores VMEM stores follow every prefetch (the prologue steps
-    // pad with dropped stores), so one unconditional wait fits every step --
-    // two waits in two branches let hipcc copy the in-flight registers ahead
-    // of the wait (tools/check_prefetch_isa.py caught it).
-    PP_WAIT(kStores, OCT0);
-    if constexpr (OCT0) {
-      PairLds0& L = *static_cast<PairLds0*>(ldsv);
-      stage_img(L, Ys + kPB);
-      fetch(Ys + 2 * kPB);
-    } else {
-      PairLdsN& L = *static_cast<PairLdsN*>(ldsv);
-      stage_src(L, buf, Ys);
-      fetch(Ys + kPB);
-    }
+    const int slot = (s + kRing) % kRing;  // s >= -2
+    // ---- this step's source rows have landed (own loads: vmcnt; the other
+    // wave's: the barrier); slot (s + 2) % 3 was read in step s - 1 ----
+    PP_WAIT(kWaitN);
     pp_barrier();
+    issue(src_row(s + 2), (s + 2 + kRing) % kRing);
     if constexpr (OCT0) {
       PairLds0& L = *static_cast<PairLds0*>(ldsv);
       // ---- base row pass: ring rows [Ys + 4, Ys + 8) ----
       if (t < kPB * (kBC / 4)) {
         const int j = t / (kBC / 4), i = t - j * (kBC / 4);
-        const float4* p = reinterpret_cast<const float4*>(&L.img[j][4 * i]);
+        const float4* p = reinterpret_cast<const float4*>(&L.img[slot][j][4 * i]);
         float v[12];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
@@ -487,14 +456,14 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
     } else {
       PairLdsN& L = *static_cast<PairLdsN*>(ldsv);
       hbuf = L.h[wv];
-      brow = &L.base[buf][lane >> 4][4 * (lane & 15)];
+      brow = &L.base[slot][lane >> 4][4 * (lane & 15)];
     }
     {
       const float4* p = reinterpret_cast<const float4*>(brow);
       float v[40];
 #pragma unroll
       for (int q = 0; q < 10; ++q) {
-        const float4 f = p[q];
+        const float4 f = (PP_ABL & 1) ? make_float4(lane + q, lane - q, lane * q, q) : p[q];
         v[4 * q] = f.x;
         v[4 * q + 1] = f.y;
         v[4 * q + 2] = f.z;
@@ -540,13 +509,13 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
     pp_dispatch<WA, WB>((s + kPer) % kPer, aa, ab, ha, hb, oa, ob);  // s >= -2
     pp_stores<WA, WB>(oa, ob, o);
   }
-  PP_WAIT(0, OCT0);  // the last (unused) prefetch lands before the wave ends
+  PP_WAIT(0);  // the last (unused) loads land before the wave ends
 }
 
 #undef PP_WAIT
 
 template <bool OCT0>
-__global__ __launch_bounds__(128) void pyr_pair_kernel(PairArgs A) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(PP_WPE))) void pyr_pair_kernel(PairArgs A) {
   __shared__ __attribute__((aligned(16))) char lds[OCT0 ? sizeof(PairLds0) : sizeof(PairLdsN)];
   // XCD-aware order (speed only): blocks b and b + 8 share an XCD, so XCD x
   // takes the contiguous run [x G/8, (x+1) G/8) of (image, chunk, strip) items

@@ -91,24 +91,28 @@ def flight(L, labels, i):
     return sorted(seen - waits), waits
 
 
-def min_vmem_to_waits(L, labels, i):
+def min_vmem_to_waits(L, labels, i, skip=0):
     """0-1 BFS from line i + 1: the fewest VMEM instructions (loads, stores)
-    issued on any path from the load at line i to each vmcnt wait it reaches.
-    A wait vmcnt(N) only covers the load if every path issues >= N of them."""
+    issued on any path from the load at line i to each vmcnt wait it reaches
+    after passing `skip` earlier waits (an LDS-DMA ring slot is consumed
+    `skip` steps after the one that issues it).  A wait vmcnt(N) only covers
+    the load if every path issues >= N of them."""
     from collections import deque
     best, res = {}, {}
-    dq = deque([(i + 1, 0)])
+    dq = deque([(i + 1, 0, 0)])
     while dq:
-        k, c = dq.popleft()
-        if k >= len(L) or best.get(k, 1 << 30) <= c:
+        k, c, w = dq.popleft()
+        if k >= len(L) or best.get((k, w), 1 << 30) <= c:
             continue
-        best[k] = c
+        best[(k, w)] = c
         line = L[k].strip()
         m = re.search(r's_waitcnt\s+vmcnt\((\d+)\)', line)
-        if m:
+        if m and int(m.group(1)) > 0 and w < skip:
+            w += 1
+        elif m:
             res[k] = min(res.get(k, 1 << 30), c)
             continue
-        w = 1 if re.match(r'(buffer|global)_(load|store)', line) else 0
+        wt = 1 if re.match(r'(buffer|global)_(load|store)', line) else 0
         nxt = []
         mb = re.match(r's_(c?)branch\w*\s+(\.LBB\d+_\d+)', line)
         if mb:
@@ -118,7 +122,7 @@ def min_vmem_to_waits(L, labels, i):
         elif not line.startswith('s_endpgm'):
             nxt.append(k + 1)
         for n in nxt:
-            (dq.append if w else dq.appendleft)((n, c + w))
+            (dq.append if wt else dq.appendleft)((n, c + wt, w))
     return res
 
 
@@ -145,7 +149,7 @@ def check(src, kname, method):
                 in_asm = True
             elif ';;#ASMEND' in l:
                 in_asm = False
-            elif in_asm and re.match(r'\s+global_load_dword', l):
+            elif in_asm and re.match(r'\s+(global_load_dword|buffer_load_dword.*\blds\b)', l):
                 loads.append(k)
         n = 0
         groups = {}
@@ -154,7 +158,8 @@ def check(src, kname, method):
             if not waits:
                 print(f'  {tag}: the load at line {i} reaches no vmcnt wait')
                 n += 1
-            d = regs(L[i].split()[1].rstrip(','))
+            # an LDS-DMA load writes no register (its first operand is the offset)
+            d = set() if re.search(r'\blds\b', L[i]) else regs(L[i].split()[1].rstrip(','))
             for j in span:
                 line = L[j].strip()
                 if not line or line.startswith(';') or line.startswith('.'):
@@ -167,7 +172,11 @@ def check(src, kname, method):
                     print(f'  {tag}: line {j} touches prefetch register of line {i}: {line}')
             stores = sum(1 for j in span if re.match(r'\s+(buffer|global)_store', L[j]))
             if method == 'cfg':
-                for w, c in min_vmem_to_waits(L, labels, i).items():
+                # pyramid_pair's LDS-DMA ring: a step's rows are issued two
+                # steps ahead of the wait that covers them (the vmcnt(0) at
+                # the end covers everything)
+                skip = 1 if re.search(r'\blds\b', L[i]) else 0
+                for w, c in min_vmem_to_waits(L, labels, i, skip).items():
                     need = int(re.search(r'vmcnt\((\d+)\)', L[w]).group(1))
                     if c < need:
                         n += 1
