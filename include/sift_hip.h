@@ -197,7 +197,12 @@ int sift_knn_match_l1_device(sift_ctx* ctx, const float* d_query, int n_query, c
  * defaults are ransac_thresh 3, max_iters 2000, confidence 0.995.  H is a
  * row-major 3x3 with H[8] = 1; inlier_mask (n bytes, may be NULL) gets the
  * RANSAC inliers.  Host code, no context.  SIFT_E_INVALID (H zeroed) when no
- * model is found or n < 4 -- OpenCV's empty Mat. */
+ * model is found or n < 4 -- OpenCV's empty Mat.
+ * Not bit-compatible with OpenCV: the final refinement is 10 steps of a plain
+ * Levenberg-Marquardt on H[0..7] (normal equations, Gaussian elimination), not
+ * OpenCV's LMSolver, so H can differ from cv::findHomography's in the last
+ * digits (the RANSAC sampling and inlier mask follow OpenCV's order).  Parity
+ * is pinned only against oracle/homography.py, which restates the same steps. */
 int sift_find_homography(const float* src_xy, const float* dst_xy, int n, double ransac_thresh, int max_iters,
                          double confidence, double* H, unsigned char* inlier_mask);
 int sift_perspective_transform(const double* H, const float* xy, int n, float* out_xy);
