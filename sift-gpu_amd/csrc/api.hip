@@ -30,7 +30,7 @@ Layout make_layout(int rows, int cols, int n_oct) {
     Octave& O = L.oct[o];
     O.rows = r;
     O.cols = c;
-    O.pitch = round_up(c > 0 ? c : 1, 16);
+    O.pitch = round_up(c > 0 ? c : 1, kPitchAlign);
     const long long plane = (long long)O.rows * O.pitch;
     for (int s = 0; s < kScales; ++s) O.g_off[s] = g + s * plane;
     for (int s = 0; s < kDogPer; ++s) O.d_off[s] = d + s * plane;
@@ -133,7 +133,8 @@ struct sift_ctx {
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
   std::vector<char> fast_taps;    // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip), passed by value
-  bool fast_pair = true;          // SIFT_FLAG_FAST via pyramid_pair.hip (round 3)
+  bool fast_pair = true;          // SIFT_FLAG_FAST via pyramid_pair.hip / pyramid_tri.hip (round 3)
+  bool fast_tri = true;           // pyramid_tri.hip (SIFT_HIP_FAST_PAIR=1: pyramid_pair.hip)
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
   long long small_max = 2048;
@@ -331,7 +332,10 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
           launch_decimate(st, L, o, c->d_gpyr, batch);
         }
         StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-        launch_pyramid_pair(st, L, o, c->d_gpyr, src, batch);
+        if (c->fast_tri)
+          launch_pyramid_tri(st, L, o, c->d_gpyr, src, batch);
+        else
+          launch_pyramid_pair(st, L, o, c->d_gpyr, src, batch);
       } else {
         StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
         launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
@@ -619,7 +623,7 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   *out = nullptr;
   // descriptor.hip gathers with 32-bit element offsets inside one plane
   // (row * pitch + col): an octave-0 plane must stay below 2^31 elements
-  if ((long long)max_rows * round_up(max_cols, 16) >= (1ll << 31)) return SIFT_E_SIZE;
+  if ((long long)max_rows * round_up(max_cols, kPitchAlign) >= (1ll << 31)) return SIFT_E_SIZE;
   if (hipSetDevice(device) != hipSuccess) return SIFT_E_HIP;
   sift_ctx* c = new sift_ctx();
   c->device = device;
@@ -635,7 +639,7 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(SIFT_E_HIP);
   c->own_stream = true;
   const Layout L = make_layout(max_rows, max_cols, c->max_oct);
-  c->in_pitch = round_up(max_cols, 16);
+  c->in_pitch = round_up(max_cols, kPitchAlign);
   c->in_img = c->in_pitch * max_rows;
   c->gpyr_elems = L.g_img * max_batch;
   c->dog_elems = L.d_img * max_batch;
@@ -693,6 +697,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     // host's) unless SIFT_HIP_FAST_V1=1 selects round 2's pyr_fast_kernel
     const char* e = getenv("SIFT_HIP_FAST_V1");
     c->fast_pair = pair_taps_match(c->fast_taps.data()) && !(e && atoi(e) != 0);
+    const char* ep = getenv("SIFT_HIP_FAST_PAIR");
+    c->fast_tri = !(ep && atoi(ep) != 0);
   }
   MathConsts mc;
   host_math_consts(&mc);

@@ -32,8 +32,12 @@ constexpr double kCvPi = 3.1415926535897932384626433832795;
 
 // ---- pyramid layout in HBM ------------------------------------------------
 // Per image: octave-major, 5 Gaussian planes then (separately) 4 DoG planes,
-// each plane rows x pitch floats, pitch = cols rounded up to 16 floats (64 B)
-// so every plane row starts 64-B aligned and float4 access is legal.
+// each plane rows x pitch floats, pitch = cols rounded up to 32 floats (128 B,
+// one L2 line), so every plane row, plane and image block starts on a line
+// boundary: a 64-column strip's row is two whole lines, never a partial-line
+// write.  (With 64-B pitches the 1080p image block was 55,251,520 B, an odd
+// number of half lines, so every odd image of a batch was misaligned.)
+constexpr int kPitchAlign = 32;
 struct Octave {
   int rows, cols, pitch;
   int pad_;
@@ -244,6 +248,9 @@ void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Pl
 void launch_pyramid_pair(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
 bool pyramid_pair_fuses(const Layout& L, int o);
 bool pair_taps_match(const void* coef);
+// pyramid_tri.hip (SIFT_FLAG_FAST, round 3, default): the same planes as
+// launch_pyramid_pair, three wave roles per workgroup.
+void launch_pyramid_tri(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
 
 // detect.hip
 struct DetectBufs {

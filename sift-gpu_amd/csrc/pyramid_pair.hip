@@ -67,6 +67,20 @@
 #ifndef PP_ABL
 #define PP_ABL 0
 #endif
+// Row-pass window reads issued just ahead of their first tap (fewer live
+// VGPRs) instead of all at the top of the pass.
+#ifndef PP_ROLE_ONLY  // register-count experiments only: compile one wave role
+#define PP_ROLE_ONLY 0
+#endif
+#ifndef PP_ASM_FMA
+#define PP_ASM_FMA 0
+#endif
+#ifndef PP_LAZY
+#define PP_LAZY 0
+#endif
+#ifndef PP_LAZY_D
+#define PP_LAZY_D 3
+#endif
 
 namespace sift {
 
@@ -74,6 +88,7 @@ namespace sift {
 
 namespace {
 
+constexpr int kLazyD = PP_LAZY_D;  // taps between a lazy window read and its first use
 constexpr int kPW = 64;         // output columns per strip
 constexpr int kPH = 18;         // widest scale half-width
 constexpr int kPB = 4;          // rows per step
@@ -92,7 +107,14 @@ static_assert(kIC <= 128 && kBC <= 128 && kBPit == 128, "a staged row is two 64-
 // still fit 32 bits.
 constexpr unsigned kDropV = 0x7f000000u;
 
-constexpr int kRing = 3;  // source rows in flight: steps s, s + 1 landed / landing, s + 2 issued
+// Source-row prefetch lead: step s + kLeadSteps's rows are issued in step s.
+// vmcnt also counts stores (gfx9), so waiting for a step's loads waits for
+// every store issued before them: a longer lead gives those stores more time.
+#ifndef PP_LEAD
+#define PP_LEAD 2
+#endif
+constexpr int kLeadSteps = PP_LEAD;
+constexpr int kRing = kLeadSteps + 1;  // ring slots: the step being read + the steps in flight
 struct PairLds0 {  // octave 0
   float base[2][kPB][kBPit];
   float h[2][2][kPB][kPW];  // [wave][scale][row][column]
@@ -156,7 +178,7 @@ static_assert(PScale<18>::P >= 37 && PScale<4>::P >= 9 && PScale<12>::P >= 25 &&
               "P >= 2w + 1");
 
 template <int W>
-__device__ __forceinline__ float ptap(int k) {
+__host__ __device__ constexpr float ptap(int k) {
   return W == 18 ? kFastT4[k] : W == 12 ? kFastT3[k] : W == 8 ? kFastT2[k] : kFastT1[k];
 }
 
@@ -177,6 +199,24 @@ struct PairArgs {
 
 namespace {
 
+// In-place v_fmac with the tap as a literal (PP_ASM_FMA): hipcc otherwise
+// renames accumulators through v_fmamk (dst != acc) and copies them back at
+// the phase merge, which doubles their live registers.
+template <int W, int R, int D>
+__device__ __forceinline__ void pp_fma_one(float (&acc)[PScale<W>::P], float h) {
+  constexpr int P = PScale<W>::P;
+  constexpr int slot = ((R - D) % P + P) % P;
+  constexpr unsigned bits = __builtin_bit_cast(unsigned, ptap<W>(D < 0 ? -D : D));
+  if constexpr (D == -W)
+    asm("v_mul_f32 %0, %2, %1" : "=v"(acc[slot]) : "v"(h), "n"(bits));
+  else
+    asm("v_fmac_f32 %0, %2, %1" : "+v"(acc[slot]) : "v"(h), "n"(bits));
+}
+template <int W, int R, int... I>
+__device__ __forceinline__ void pp_scatter_asm(float (&acc)[PScale<W>::P], float h, std::integer_sequence<int, I...>) {
+  (pp_fma_one<W, R, I - W>(acc, h), ...);
+}
+
 // Column pass of one source row at cycle row R: output R - d gets g_|d| h,
 // d = -W..W (slot (R - d) mod P); d = -W is that output's first term.
 template <int W, int R>
@@ -189,12 +229,17 @@ __device__ __forceinline__ void pp_scatter(float (&acc)[PScale<W>::P], float h) 
 #pragma unroll
   for (int d = -W; d <= W; ++d) {
     const int slot = ((R - d) % P + P) % P;
-    const float c = ptap<W>(d < 0 ? -d : d);
-    if (d == -W)
-      acc[slot] = c * h;
-    else
-      acc[slot] = fmaf(c, h, acc[slot]);
+    if constexpr (PP_ASM_FMA) {
+      (void)slot;  // pp_scatter_asm below
+    } else {
+      const float c = ptap<W>(d < 0 ? -d : d);
+      if (d == -W)
+        acc[slot] = c * h;
+      else
+        acc[slot] = fmaf(c, h, acc[slot]);
+    }
   }
+  if constexpr (PP_ASM_FMA) pp_scatter_asm<W, R>(acc, h, std::make_integer_sequence<int, 2 * W + 1>{});
 }
 
 struct PPOut {
@@ -348,28 +393,33 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
       pp_dma(pp_lds_addr(dst + 64), voff[1], rsrc, soff);
     }
   };
-  constexpr int kLoads = 4;                   // DMA loads per wave per step
-  constexpr int kWaitN = 2 * kStores + kLoads;  // VMEM operations after a step's loads at its wait
+  constexpr int kLoads = 4;  // DMA loads per wave per step
+  // VMEM operations younger than a step's loads at its wait: the stores of
+  // kLeadSteps steps and the loads of kLeadSteps - 1
+  constexpr int kWaitN = kLeadSteps * kStores + (kLeadSteps - 1) * kLoads;
+  static_assert(kWaitN <= 63, "vmcnt is 6 bits");
   // source rows of step t: the image rows its base row pass needs (octave 0)
   // or its base rows (octave > 0)
   auto src_row = [&](int t) { return Ystart + kPB * t + (OCT0 ? kPB : 0); };
 
   const int s0 = OCT0 ? -2 : 0;
-  // steps s0 and s0 + 1 in flight, each followed by kStores dropped stores so
-  // every wait below sees exactly kWaitN younger operations
-  issue(src_row(s0), (s0 + kRing) % kRing);
-  pp_pad<kStores>(r0);
-  issue(src_row(s0 + 1), (s0 + 1 + kRing) % kRing);
-  pp_pad<kStores>(r0);
+  auto ring_slot = [](int t) { return (t + 4 * kRing) % kRing; };  // t >= -2
+  // steps s0 .. s0 + kLeadSteps - 1 in flight, each followed by kStores
+  // dropped stores so every wait below sees exactly kWaitN younger operations
+#pragma unroll
+  for (int i = 0; i < kLeadSteps; ++i) {
+    issue(src_row(s0 + i), ring_slot(s0 + i));
+    pp_pad<kStores>(r0);
+  }
   for (int s = s0; s < nsteps; ++s) {
     const int Ys = Ystart + kPB * s;
     const int buf = s & 1;
-    const int slot = (s + kRing) % kRing;  // s >= -2
+    const int slot = ring_slot(s);
     // ---- this step's source rows have landed (own loads: vmcnt; the other
-    // wave's: the barrier); slot (s + 2) % 3 was read in step s - 1 ----
+    // wave's: the barrier); slot (s + kLeadSteps) % kRing was read in step s - 1 ----
     PP_WAIT(kWaitN);
     pp_barrier();
-    issue(src_row(s + 2), (s + 2 + kRing) % kRing);
+    issue(src_row(s + kLeadSteps), ring_slot(s + kLeadSteps));
     if constexpr (OCT0) {
       PairLds0& L = *static_cast<PairLds0*>(ldsv);
       // ---- base row pass: ring rows [Ys + 4, Ys + 8) ----
@@ -460,30 +510,50 @@ __device__ __forceinline__ void pp_walk(const PairArgs& A, void* ldsv, int wv, i
     }
     {
       const float4* p = reinterpret_cast<const float4*>(brow);
-      float v[40];
+      // The role's window [kPH - WA, kPH + 3 + WA] in whole 16-B reads (every
+      // component kept live, so hipcc cannot narrow a read to a misaligned
+      // ds_read2_b64: 2-way bank conflicts).  PP_LAZY: each read is issued
+      // kLazyD taps before the tap that first needs it and a chunk dies with
+      // its last tap, so ~16 window registers are live instead of 40.
+      float4 ch[10];
+      constexpr int qlo = (kPH - WA) / 4, qhi = (kPH + 3 + WA) / 4;
+      auto first_tap = [](int q) {  // first tap k whose pair sums read chunk q
+        int m = 1 << 20;
+        for (int e = 4 * q; e < 4 * q + 4; ++e) m = min(m, e < kPH ? kPH - e : max(e - kPH - 3, 0));
+        return m;
+      };
+      auto load = [&](int q) {
+        float4 f = (PP_ABL & 1) ? make_float4(lane + q, lane - q, lane * q, q) : p[q];
+        asm("" : "+v"(f.x), "+v"(f.y), "+v"(f.z), "+v"(f.w));
+        ch[q] = f;
+      };
+      auto loads_at = [&](int k) {  // the reads due at tap k
 #pragma unroll
-      for (int q = 0; q < 10; ++q) {
-        const float4 f = (PP_ABL & 1) ? make_float4(lane + q, lane - q, lane * q, q) : p[q];
-        v[4 * q] = f.x;
-        v[4 * q + 1] = f.y;
-        v[4 * q + 2] = f.z;
-        v[4 * q + 3] = f.w;
-      }
+        for (int q = qlo; q <= qhi; ++q)
+          if (PP_LAZY ? max(first_tap(q) - kLazyD, 0) == k : k == 0) load(q);
+        if (PP_LAZY) asm volatile("" ::: "memory");  // no hoisting across taps
+      };
+      auto v = [&](int e) -> float {
+        const float4& c = ch[e >> 2];
+        return (e & 3) == 0 ? c.x : (e & 3) == 1 ? c.y : (e & 3) == 2 ? c.z : c.w;
+      };
       // k outer, the 4 columns inner: the 4 pair sums of a tap, then the 8
       // fma of the 8 chains -- every instruction's operands were produced >= 4
       // instructions earlier (column-outer order made hipcc issue each fma
       // right behind the add or fma it depends on: 0.44 of the VALU issue rate)
+      loads_at(0);
       float ha[4], hb[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        ha[u] = ptap<WA>(0) * v[kPH + u];
-        hb[u] = ptap<WB>(0) * v[kPH + u];
+        ha[u] = ptap<WA>(0) * v(kPH + u);
+        hb[u] = ptap<WB>(0) * v(kPH + u);
       }
 #pragma unroll
       for (int k = 1; k <= WA; ++k) {
+        loads_at(k);
         float pk[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) pk[u] = v[kPH + u - k] + v[kPH + u + k];
+        for (int u = 0; u < 4; ++u) pk[u] = v(kPH + u - k) + v(kPH + u + k);
         asm volatile("" : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]), "+v"(pk[3]));
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -528,10 +598,16 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(PP_WPE))) v
   const int ck = rest % A.chunks, b = rest / A.chunks;
   const int x0 = strip * kPW, y0 = ck * A.chunk, y1 = min(y0 + A.chunk, A.rows);
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if PP_ROLE_ONLY == 1
+  pp_walk<OCT0, 18, 4>(A, lds, wv, b, x0, y0, y1);
+#elif PP_ROLE_ONLY == 2
+  pp_walk<OCT0, 12, 8>(A, lds, wv, b, x0, y0, y1);
+#else
   if (wv == 0)
     pp_walk<OCT0, 18, 4>(A, lds, 0, b, x0, y0, y1);
   else
     pp_walk<OCT0, 12, 8>(A, lds, 1, b, x0, y0, y1);
+#endif
 }
 
 }  // namespace

@@ -1,5 +1,6 @@
 """GPU tests of SIFT_FLAG_FAST: the separable row/column Gaussian pyramid
-(sift-gpu_amd/csrc/pyramid_fast.hip) in front of the exact downstream kernels.
+(sift-gpu_amd/csrc/pyramid_tri.hip; pyramid_pair.hip and pyramid_fast.hip
+behind switches) in front of the exact downstream kernels.
 
 Fast mode is NOT bit-exact with the reference's 2-D float chain
 (src/sift.cpp:137-146): it applies K[a][b] = 8192 g(a) g(b) as a row pass and
@@ -33,22 +34,48 @@ def fctx(siftgpu):
     c.close()
 
 
-@pytest.fixture(scope="module", params=["pair", "v1"])
-def fctx_both(request, siftgpu):
-    """Both SIFT_FLAG_FAST pyramids: pyramid_pair.hip (default, round 3) and
-    round 2's pyramid_fast.hip (SIFT_HIP_FAST_V1=1, read at context creation)."""
+def _fast_ctx(siftgpu, kind, rows=1080, cols=1920, batch=4):
+    """A SIFT_FLAG_FAST context on one of the three separable pyramids:
+    pyramid_tri.hip (default, round 3), pyramid_pair.hip (SIFT_HIP_FAST_PAIR=1)
+    and round 2's pyramid_fast.hip (SIFT_HIP_FAST_V1=1); the switches are read
+    at context creation."""
     import os
-    old = os.environ.pop("SIFT_HIP_FAST_V1", None)
-    if request.param == "v1":
-        os.environ["SIFT_HIP_FAST_V1"] = "1"
+    env = {"tri": {}, "pair": {"SIFT_HIP_FAST_PAIR": "1"}, "v1": {"SIFT_HIP_FAST_V1": "1"}}[kind]
+    keys = ("SIFT_HIP_FAST_PAIR", "SIFT_HIP_FAST_V1")
+    old = {k: os.environ.pop(k, None) for k in keys}
+    os.environ.update(env)
     try:
-        c = siftgpu.Context(1080, 1920, 4, device=0, flags=FAST)
+        return siftgpu.Context(rows, cols, batch, device=0, flags=FAST)
     finally:
-        os.environ.pop("SIFT_HIP_FAST_V1", None)
-        if old is not None:
-            os.environ["SIFT_HIP_FAST_V1"] = old
+        for k in keys:
+            os.environ.pop(k, None)
+            if old[k] is not None:
+                os.environ[k] = old[k]
+
+
+@pytest.fixture(scope="module", params=["tri", "pair", "v1"])
+def fctx_both(request, siftgpu):
+    c = _fast_ctx(siftgpu, request.param)
     yield c
     c.close()
+
+
+@pytest.mark.parametrize("shape,b", [((1080, 1920), 0), ((203, 157), 2), ((33, 1200), 12), ((540, 960), 5)])
+def test_fast_tri_equals_pair(siftgpu, oracle, shape, b):
+    """pyramid_tri.hip and pyramid_pair.hip apply the same row-pass chains and the
+    same in-order column scatter, so their planes are bit-identical."""
+    img = oracle.synth_image(b, *shape)
+    t = _fast_ctx(siftgpu, "tri", *shape, 1)
+    p = _fast_ctx(siftgpu, "pair", *shape, 1)
+    try:
+        gt = t.buildGaussianPyramid(img, 5)
+        gp = p.buildGaussianPyramid(img, 5)
+    finally:
+        t.close()
+        p.close()
+    assert len(gt) == len(gp)
+    for i, (a, c) in enumerate(zip(gt, gp)):
+        assert a.tobytes() == c.tobytes(), f"plane {i} differs"
 
 
 @pytest.mark.parametrize("shape,b", [((1080, 1920), 0), ((203, 157), 2), ((33, 1200), 12),

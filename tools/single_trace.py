@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""configs[1] single-image loop for kernel traces: one 1080p image resident in
+HBM, 4 octaves, sift_detect_compute_batch(batch 1) (graph replay) + sift_sync,
+--reps times; prints the median latency.
+  rocprofv3 --kernel-trace --stats -d <dir> -o run -- python3 tools/single_trace.py"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sift-gpu_amd"))
+import siftgpu  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--flags", type=int, default=0)
+    a = p.parse_args()
+    R, C = 1080, 1920
+    with siftgpu.Context(R, C, 1, device=0) as ctx:
+        ctx.set_octaves(4)
+        ctx.set_flags(a.flags)
+        img = torch.empty((1, R, C), dtype=torch.float32, device="cuda")
+        ctx.synth_images(img.data_ptr(), 1, R, C, C, R * C, seed_base=0)
+        cap = 40000
+        kpts = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
+        desc = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
+        offs = torch.empty((2,), dtype=torch.int32, device="cuda")
+        ts = []
+        for i in range(a.reps + 3):
+            t0 = time.perf_counter()
+            ctx.detect_compute_batch(img.data_ptr(), 1, R, C, C, R * C, kpts.data_ptr(), desc.data_ptr(), cap,
+                                     offs.data_ptr())
+            ctx.sync()
+            if i >= 3:
+                ts.append(time.perf_counter() - t0)
+        print(f'{{"latency_ms": {np.median(ts) * 1e3:.4f}, "keypoints": {int(offs[1].item())}}}', flush=True)
+
+
+if __name__ == "__main__":
+    main()
