@@ -738,26 +738,39 @@ def exact_block(a, world, B, R, C, S, res, tr):
     return out
 
 
+def fast_kernel():
+    """The SIFT_FLAG_FAST pyramid the library selects (sift-gpu_amd/csrc/api.hip,
+    read at context creation): pyramid_tri.hip unless a switch names another."""
+    def on(k):
+        return os.environ.get(k, "0") not in ("", "0")
+    if on("SIFT_HIP_FAST_V1"):
+        return "pyr_fast_kernel", "pyramid_fast.hip"
+    if on("SIFT_HIP_FAST_PAIR"):
+        return "pyr_pair_kernel", "pyramid_pair.hip"
+    return "pyr_tri_kernel", "pyramid_tri.hip"
+
+
 def fast_block(a, world, B, R, C, fast_res, tr):
     (fdt, _, fkp), fast_prof = fast_res
+    kname, kfile = fast_kernel()
     fst = fast_prof[1]
     mpix = world * B * R * C * a.steps / 1e6
     pf = fst.get("pyramid_fast", {"ms": 0.0, "bytes": 0.0, "launches": 0})
     gbs = pf["bytes"] / (pf["ms"] * 1e-3) / 1e9 if pf["ms"] else 0.0
-    traffic, tsrc = traffic_of(tr, "pyr_fast_kernel")
+    traffic, tsrc = traffic_of(tr, kname)
     fm = {
         "value": round(mpix / fdt, 2), "unit": "Mpix/s", "ms_per_step": round(fdt / a.steps * 1e3, 3),
         "keypoints_per_s": round(fkp * a.steps / fdt, 1), "keypoints_per_step": int(fkp),
         "stages_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in fst.items()},
         "note": "the exact leg's stream split (--streams), graph replay; SIFT_FLAG_FAST: separable row/column "
-                "Gaussian pyramid (pyramid_fast.hip) in front of the same exact DoG/extrema/orientation/"
+                f"Gaussian pyramid ({kfile}) in front of the same exact DoG/extrema/orientation/"
                 "descriptor kernels; not bit-exact (float rounding of the pyramid), keypoint/descriptor "
                 "match rates vs the CPU path are in tests/test_gpu_fast.py"}
     roof = {
         "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
         "traffic_algorithmic": round(pf["bytes"] / max(pf["launches"], 1)),
-        "traffic_source": tsrc, "kernel": "pyr_fast_kernel",
+        "traffic_source": tsrc, "kernel": kname,
         "avg_launch_ms": round(pf["ms"] / max(pf["launches"], 1), 4),
         "pyramid_ms_per_step": round(pf["ms"] / a.steps, 4),
         "note": "algorithmic bytes B_pyr = 24 B x sum of octave pixels (1 read + 5 plane writes, "

@@ -20,7 +20,7 @@ for k, v in sorted(byname.items(), key=lambda kv: -sum(kv[1])):
     print(f"  {k[0]:60s} grid {k[1]:9d}  n {len(v)}  avg {sum(v)/len(v):9.1f} us")
 counters = defaultdict(dict)   # (pass, dispatch) -> name -> value
 meta = {}
-for p in ("sq1", "sq2", "gr", "fe", "wr"):
+for p in ("sq1", "sq2", "gr", "fe", "wr", "ic"):
     f = glob.glob(os.path.join(d, p, "*counter_collection.csv"))
     if not f:
         continue
@@ -64,4 +64,6 @@ for g in sorted(agg, reverse=True):
         out["fetch_MB_x2"] = round(2 * a["FETCH_SIZE"] / 1e3, 1)   # KB -> MB, x2 gfx950 streaming calibration
     if "WRITE_SIZE" in a:
         out["write_MB"] = round(a["WRITE_SIZE"] / 1e3, 1)
+    if "SQC_ICACHE_MISSES" in a:
+        out["icache_miss_frac"] = round(a["SQC_ICACHE_MISSES"] / max(a["SQC_ICACHE_HITS"] + a["SQC_ICACHE_MISSES"], 1), 4)
     print(out)

@@ -17,4 +17,5 @@ run sq2 240 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 run gr 240 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -T --kernel-include-regex "$RE" -d $O/gr -o run --output-format csv
 run fe 240 --kernel-trace --pmc FETCH_SIZE -T --kernel-include-regex "$RE" -d $O/fe -o run --output-format csv
 run wr 240 --kernel-trace --pmc WRITE_SIZE -T --kernel-include-regex "$RE" -d $O/wr -o run --output-format csv
+[ -n "$ICACHE" ] && run ic 240 --kernel-trace --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES -T --kernel-include-regex "$RE" -d $O/ic -o run --output-format csv
 echo "prof_fast $TAG done"
