@@ -39,6 +39,10 @@
 #ifndef PT_WPE
 #define PT_WPE 5
 #endif
+// rows per step (4 or 8); 8 halves the barriers and LDS round trips per row
+#ifndef PT_ROWS
+#define PT_ROWS 8
+#endif
 // 1: each workgroup walks an equal share of the batch's (column strip, row)
 // work, split into pieces at strip ends (about 2.5 pieces of ~1350 rows per
 // workgroup for octave 0 of 64 x 1080p); 0: one fixed row chunk per workgroup
@@ -60,18 +64,20 @@ namespace {
 
 constexpr int kTW = 64;               // output columns per strip
 constexpr int kTH = 18;               // widest half-width
-constexpr int kTB = 4;                // rows per step
-constexpr int kTLead = 20;            // rows walked above the chunk (>= kTH, multiple of kTB)
+constexpr int kTB = PT_ROWS;          // rows per step
+static_assert(kTB == 4 || kTB == 8, "rows per step");
+constexpr int kTLead = kTB == 4 ? 20 : 24;  // rows walked above the chunk (>= kTH + 2, multiple of kTB)
 constexpr int kTBC = kTW + 2 * kTH;   // 100 base columns per strip: [x0 - 18, x0 + 82)
 constexpr int kTPit = 128;            // staged row pitch (floats)
-constexpr int kTHbRows = 12;          // octave-0 base row-pass ring: rows [Y - 4, Y + 8)
+constexpr int kTHbRows = kTB + 8;     // octave-0 base row-pass ring: rows [Y - 4, Y + kTB + 4)
 constexpr int kTHbPit = 100;
-constexpr int kTRing = 3;             // source rows: step s landed, s + 1 landing, s + 2 issued
+constexpr int kTLd = kTB == 4 ? 2 : 1;  // source-row prefetch lead (steps): 8 rows either way
+constexpr int kTRing = kTLd + 1;      // source-row ring slots: the step being read + the steps in flight
 constexpr int kTDropP = 0x7ffffff0;   // a buffer offset past every plane
 constexpr unsigned kTDropV = 0x7f000000u;  // one store-offset part past every plane (caller checks)
 
 struct TriLds0 {  // octave 0
-  float base[2][kTB][kTPit];       // base rows [Ys, Ys + 4), columns [x0 - 18, x0 + 110)
+  float base[kTB][kTPit];          // base rows [Ys, Ys + kTB), columns [x0 - 18, x0 + 110)
   float h[4][kTB][kTW];            // row-pass output [scale: w18, w12, w8, w4][row][column]
   float img[kTRing][kTB][kTPit];   // image rows, LDS-DMA ring (columns [x0 - 22, x0 + 106))
   float hb[kTHbRows][kTHbPit];     // base row-pass ring
@@ -128,21 +134,25 @@ __host__ __device__ constexpr float ttap(int k) {
 // cycle, planes, h-buffer slots; io = loads the source rows and runs the
 // octave-0 base passes.
 template <int ROLE> struct TRole;
+// P: the smallest multiple of kTB that is >= 2w + 1 (role 2's two scales
+// share the cycle of the larger); NC = P / kTB steps per slot cycle.
 template <> struct TRole<0> {
-  static constexpr int W1 = 18, W2 = 0, P1 = 40, P2 = 1, NC = 10, pl1 = 4, pl2 = 0, h1 = 0, h2 = 0;
+  static constexpr int W1 = 18, W2 = 0, P1 = 40, P2 = 1, NC = P1 / kTB, pl1 = 4, pl2 = 0, h1 = 0, h2 = 0;
   static constexpr bool io = false;
 };
 template <> struct TRole<1> {
-  static constexpr int W1 = 12, W2 = 0, P1 = 28, P2 = 1, NC = 7, pl1 = 3, pl2 = 0, h1 = 1, h2 = 0;
+  static constexpr int W1 = 12, W2 = 0, P1 = kTB == 4 ? 28 : 32, P2 = 1, NC = P1 / kTB, pl1 = 3, pl2 = 0, h1 = 1,
+                       h2 = 0;
   static constexpr bool io = true;
 };
 template <> struct TRole<2> {
-  static constexpr int W1 = 8, W2 = 4, P1 = 20, P2 = 10, NC = 5, pl1 = 2, pl2 = 1, h1 = 2, h2 = 3;
+  static constexpr int W1 = 8, W2 = 4, P1 = kTB == 4 ? 20 : 24, P2 = kTB == 4 ? 10 : 12, NC = P1 / kTB, pl1 = 2,
+                       pl2 = 1, h1 = 2, h2 = 3;
   static constexpr bool io = true;
 };
-static_assert(4 * TRole<0>::NC % TRole<0>::P1 == 0 && TRole<0>::P1 >= 37, "role 0 cycle");
-static_assert(4 * TRole<1>::NC % TRole<1>::P1 == 0 && TRole<1>::P1 >= 25, "role 1 cycle");
-static_assert(4 * TRole<2>::NC % TRole<2>::P1 == 0 && 4 * TRole<2>::NC % TRole<2>::P2 == 0 &&
+static_assert(kTB * TRole<0>::NC % TRole<0>::P1 == 0 && TRole<0>::P1 >= 37, "role 0 cycle");
+static_assert(kTB * TRole<1>::NC % TRole<1>::P1 == 0 && TRole<1>::P1 >= 25, "role 1 cycle");
+static_assert(kTB * TRole<2>::NC % TRole<2>::P1 == 0 && kTB * TRole<2>::NC % TRole<2>::P2 == 0 &&
                   TRole<2>::P1 >= 17 && TRole<2>::P2 >= 9,
               "role 2 cycle");
 static_assert(TRole<2>::pl1 == kLayers, "the decimated plane (nOctaveLayers) is role 2's first scale");
@@ -252,9 +262,9 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
   constexpr bool kIO = R_::io, kDec = ROLE == 2;
   // VMEM stores per step: octave-0 base column pass (4, io roles), 1 per row
   // and scale, + 1 per row for the decimated plane
-  constexpr int kStores = (PT_ABL & 1) ? 0 : (OCT0 && kIO ? 4 : 0) + kTB * ((W2 ? 2 : 1) + (kDec ? 1 : 0));
-  constexpr int kLoads = kIO ? 4 : 0;  // LDS-DMA loads per step (two rows of four)
-  constexpr int kWaitN = 2 * kStores + kLoads;
+  constexpr int kStores = (PT_ABL & 1) ? 0 : (OCT0 && kIO ? kTB : 0) + kTB * ((W2 ? 2 : 1) + (kDec ? 1 : 0));
+  constexpr int kLoads = kIO ? kTB : 0;  // LDS-DMA loads per step (half the step's rows, two per row)
+  constexpr int kWaitN = kTLd * kStores + (kTLd - 1) * kLoads;
   static_assert(kWaitN <= 63, "vmcnt is 6 bits");
   const int t = threadIdx.x, lane = t & 63;
   float* const gimg = A.gpyr + b * A.g_img;
@@ -278,8 +288,8 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
 #pragma unroll
   for (int k = 0; k < P2; ++k) a2[k] = 0.f;
 
-  // Source staging (io roles): role 1 loads rows 0, 1 of a step's four, role
-  // 2 rows 2, 3, each as two 64-lane LDS-DMA loads (columns c0 + lane,
+  // Source staging (io roles): role 1 loads the first half of a step's rows,
+  // role 2 the second, each row as two 64-lane LDS-DMA loads (columns c0 + lane,
   // c0 + 64 + lane; c0 = x0 - 22 for the image, x0 - 18 for plane 0).
   const int c0 = OCT0 ? x0 - 22 : x0 - kTH;
   unsigned voff[2];
@@ -289,11 +299,12 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
     voff[hh] = (c >= 0 && c < cols - 1) ? (unsigned)c * 4u : kTDropV;
   }
   const TRsrc rsrc = pt_rsrc(const_cast<float*>(src), (long long)rows * A.s_pitch * 4);
-  const int rw = 2 * (ROLE - 1);
+  constexpr int kHalf = kTB / 2;
+  const int rw = kHalf * (ROLE - 1);
   float* const ring = OCT0 ? &static_cast<TriLds0*>(ldsv)->img[0][0][0] : &static_cast<TriLdsN*>(ldsv)->base[0][0][0];
   auto issue = [&](int r0_, int sl) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kHalf; ++i) {
       const int r = r0_ + rw + i;
       const unsigned soff = (r >= 0 && r < rows - 1) ? (unsigned)(r * A.s_pitch * 4) : kTDropV;
       float* dst = ring + (sl * kTB + rw + i) * kTPit;
@@ -301,14 +312,19 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
       pt_dma(pt_lds_addr(dst + 64), voff[1], rsrc, soff);
     }
   };
-  auto src_row = [&](int s) { return Ystart + kTB * s + (OCT0 ? kTB : 0); };
-  auto ring_slot = [](int s) { return (s + 4 * kTRing) % kTRing; };  // s >= -2
-  const int s0 = OCT0 ? -2 : 0;
+  // octave 0: step s's base row pass makes base row-pass rows [Ys + 4,
+  // Ys + 4 + kTB) from these image rows; octave > 0: the step's base rows
+  auto src_row = [&](int s) { return Ystart + kTB * s + (OCT0 ? 4 : 0); };
+  auto ring_slot = [](int s) { return (s + 4 * kTRing) % kTRing; };  // s >= s0
+  const int s0 = OCT0 ? -(8 / kTB) : 0;  // octave 0: the steps that fill the base ring
+  // ring position of base row-pass row Ystart + r (r >= -16)
+  auto hb_pos = [](int r) { return (r + 8 * kTHbRows) % kTHbRows; };
   if constexpr (kIO) {
-    issue(src_row(s0), ring_slot(s0));
-    pt_pad<kStores>(r0);
-    issue(src_row(s0 + 1), ring_slot(s0 + 1));
-    pt_pad<kStores>(r0);
+#pragma unroll
+    for (int i = 0; i < kTLd; ++i) {
+      issue(src_row(s0 + i), ring_slot(s0 + i));
+      pt_pad<kStores>(r0);
+    }
   }
   const int bt = t - 64;  // io roles: thread index over waves 1 and 2
   int s = s0;
@@ -320,40 +336,45 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
     constexpr int M = decltype(Mc)::value;
     if (s >= nsteps) return false;
     const int Ys = Ystart + kTB * s;
-    const int buf = s & 1;
     const int slot = ring_slot(s);
     if constexpr (kIO) PT_WAIT(kWaitN);  // own loads of step s; the other role's: the barrier
     pt_barrier();
-    if constexpr (kIO) issue(src_row(s + 2), ring_slot(s + 2));
+    if constexpr (kIO) issue(src_row(s + kTLd), ring_slot(s + kTLd));
     if constexpr (OCT0) {
       TriLds0& L = *static_cast<TriLds0*>(ldsv);
-      // ---- base row pass (createInitialImage, w = 4): ring rows [Ys + 4, Ys + 8) ----
-      if (kIO && bt < kTB * (kTBC / 4)) {
-        const int j = bt / (kTBC / 4), i = bt - j * (kTBC / 4);
-        const float4* p = reinterpret_cast<const float4*>(&L.img[slot][j][4 * i]);
-        float v[12];
+      // ---- base row pass (createInitialImage, w = 4): ring rows [Ys + 4, Ys + 4 + kTB) ----
+      if constexpr (kIO) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const float4 f = p[q];
-          v[4 * q] = f.x;
-          v[4 * q + 1] = f.y;
-          v[4 * q + 2] = f.z;
-          v[4 * q + 3] = f.w;
+        for (int it0 = 0; it0 < kTB * (kTBC / 4); it0 += 128) {
+          const int it = it0 + bt;
+          if (it < kTB * (kTBC / 4)) {
+            const int j = it / (kTBC / 4), i = it - j * (kTBC / 4);
+            const float4* p = reinterpret_cast<const float4*>(&L.img[slot][j][4 * i]);
+            float v[12];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+              const float4 f = p[q];
+              v[4 * q] = f.x;
+              v[4 * q + 1] = f.y;
+              v[4 * q + 2] = f.z;
+              v[4 * q + 3] = f.w;
+            }
+            float hv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) hv[u] = kFastT0[0] * v[4 + u];
+#pragma unroll
+            for (int k = 1; k <= 4; ++k) {
+              float pk[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) pk[u] = v[4 + u - k] + v[4 + u + k];
+              asm volatile("" : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]), "+v"(pk[3]));
+#pragma unroll
+              for (int u = 0; u < 4; ++u) hv[u] = fmaf(kFastT0[k], pk[u], hv[u]);
+            }
+            const int hs = hb_pos(kTB * s + 4 + j);
+            *reinterpret_cast<float4*>(&L.hb[hs][4 * i]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+          }
         }
-        float hv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) hv[u] = kFastT0[0] * v[4 + u];
-#pragma unroll
-        for (int k = 1; k <= 4; ++k) {
-          float pk[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) pk[u] = v[4 + u - k] + v[4 + u + k];
-          asm volatile("" : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]), "+v"(pk[3]));
-#pragma unroll
-          for (int u = 0; u < 4; ++u) hv[u] = fmaf(kFastT0[k], pk[u], hv[u]);
-        }
-        const int hs = (kTB * (s + 3) + j) % kTHbRows;  // ring slot of row Ys + 4 + j (s >= -2)
-        *reinterpret_cast<float4*>(&L.hb[hs][4 * i]) = make_float4(hv[0], hv[1], hv[2], hv[3]);
       }
       pt_barrier();
       // ---- base column pass: base rows [Ys, Ys + 4) -> plane 0 + the LDS base rows ----
@@ -361,10 +382,10 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
       // column), so each io wave issues exactly 4 stores here.
       if constexpr (kIO) {
         const int tc = min(bt, kTBC - 1);
-        const int q0 = (kTB * s + 4) % kTHbRows;  // slot of ring row Ys - 4
-        float hv[12];
+        const int q0 = hb_pos(kTB * s - 4);  // ring row Ys - 4
+        float hv[kTB + 8];
 #pragma unroll
-        for (int q = 0; q < 12; ++q) {
+        for (int q = 0; q < kTB + 8; ++q) {
           const int sl = q0 + q;
           hv[q] = L.hb[sl >= kTHbRows ? sl - kTHbRows : sl][tc];
         }
@@ -387,33 +408,35 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
         for (int j = 0; j < kTB; ++j) {
           const int y = Ys + j;
           pt_store(r0, v0, (y >= y0 && y < y1) ? (unsigned)y * pitch4 : kTDropV, bv[j]);
-          if (bt < kTPit) L.base[buf][j][bt] = (cpad && y >= 0 && y < rows - 1) ? bv[j] : 0.f;
+          if (bt < kTPit) L.base[j][bt] = (cpad && y >= 0 && y < rows - 1) ? bv[j] : 0.f;
         }
       }
       pt_barrier();
     }
     // ---- row pass of the role's scales: h rows [Ys, Ys + 4) ----
     float (*hbuf)[kTB][kTW];
-    const float* brow;
+    const float* brow;  // row lane >> 4 of the step's base rows, columns from 4 (lane & 15)
     if constexpr (OCT0) {
       TriLds0& L = *static_cast<TriLds0*>(ldsv);
       hbuf = L.h;
-      brow = &L.base[buf][lane >> 4][4 * (lane & 15)];
+      brow = &L.base[lane >> 4][4 * (lane & 15)];
     } else {
       TriLdsN& L = *static_cast<TriLdsN*>(ldsv);
       hbuf = L.h;
       brow = &L.base[slot][lane >> 4][4 * (lane & 15)];
     }
-    {
+    // ---- row pass of the role's scales (lane = row, 4 columns; rows
+    // lane >> 4 + r4) into the wave's own h rows, read back as lane = column ----
+#pragma unroll
+    for (int r4 = 0; r4 < kTB; r4 += 4) {
       float h1[4], h2[4];
-      pt_rows<W1, W2>(brow, h1, h2);
-      const int j = lane >> 4, i = lane & 15;
+      pt_rows<W1, W2>(brow + r4 * kTPit, h1, h2);
+      const int j = (lane >> 4) + r4, i = lane & 15;
       *reinterpret_cast<float4*>(&hbuf[R_::h1][j][4 * i]) = make_float4(h1[0], h1[1], h1[2], h1[3]);
       if constexpr (W2 != 0)
         *reinterpret_cast<float4*>(&hbuf[R_::h2][j][4 * i]) = make_float4(h2[0], h2[1], h2[2], h2[3]);
     }
     pt_wave_sync();
-    // ---- column pass: lane = column; phase M of the role's slot cycle ----
     float c1[kTB], c2[kTB];
 #pragma unroll
     for (int j = 0; j < kTB; ++j) {
@@ -421,6 +444,7 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
       if constexpr (W2 != 0) c2[j] = hbuf[R_::h2][j][lane];
     }
     pt_wave_sync();
+    // ---- column pass: lane = column; phase M of the role's slot cycle ----
     float o1[kTB], o2[kTB];
     pt_col<W1, P1, M>(a1, c1, o1, std::make_integer_sequence<int, kTB>{});
     if constexpr (W2 != 0) pt_col<W2, P2, M>(a2, c2, o2, std::make_integer_sequence<int, kTB>{});
