@@ -135,6 +135,7 @@ struct sift_ctx {
   std::vector<char> fast_taps;    // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip), passed by value
   bool fast_pair = true;          // SIFT_FLAG_FAST via pyramid_pair.hip / pyramid_tri.hip (round 3)
   bool fast_tri = true;           // pyramid_tri.hip (SIFT_HIP_FAST_PAIR=1: pyramid_pair.hip)
+  bool fuse_dec = true;           // 2-D tile blurs write the next plane 0 (SIFT_HIP_FUSE_DEC=0: decimate_kernel)
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
   long long small_max = 2048;
@@ -358,9 +359,13 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       launch_blur_plane(st, c->w_base, c->d_coef + c->coef_base_off, src, c->d_gpyr + L.oct[0].g_off[0],
                         L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
   }
+  // The 2-D tile and small-tile blurs also write the next octave's plane 0
+  // when it is an exact half (no decimation launch; the launches of one image
+  // are latency-bound); the scatter form leaves it to decimate_kernel.
+  bool fused = false;  // this octave's plane 0 came out of the previous launch
   for (int o = 0; o < L.n_oct; ++o) {
     const double px = plane_px(L, o) * batch;
-    if (o > 0) {
+    if (o > 0 && !fused) {
       StageScope s(c, ST_DECIMATE, 0, 8.0 * px);
       launch_decimate(st, L, o, c->d_gpyr, batch);
     }
@@ -368,13 +373,15 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       double taps = 0;
       for (int q = 0; q < 4; ++q) taps += (double)(2 * c->wsz[q] + 1) * (2 * c->wsz[q] + 1);
       const bool sym = use_sym_blur(c, L.oct[o].rows, L.oct[o].cols, batch);
+      const bool fuse = !sym && c->fuse_dec && o + 1 < L.n_oct && blur_fuses_decimation(L, o + 1);
       StageScope s(c, sym ? ST_BLUR_SYM : ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
       if (sym)
         launch_blur_octave_sym(st, L, o, c->d_gpyr, batch);
       else if (blur_octave_tiles(L, o, batch) < c->small_max)
-        launch_blur_octave_small(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch);
+        launch_blur_octave_small(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch, fuse);
       else
-        launch_blur_octave(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch);
+        launch_blur_octave(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch, fuse);
+      fused = fuse;
     }
     if (with_dog) {
       StageScope s(c, ST_DOG, 4.0 * px, 36.0 * px);
@@ -699,6 +706,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     c->fast_pair = pair_taps_match(c->fast_taps.data()) && !(e && atoi(e) != 0);
     const char* ep = getenv("SIFT_HIP_FAST_PAIR");
     c->fast_tri = !(ep && atoi(ep) != 0);
+    const char* fd = getenv("SIFT_HIP_FUSE_DEC");
+    c->fuse_dec = !(fd && atoi(fd) == 0);
   }
   MathConsts mc;
   host_math_consts(&mc);

@@ -65,11 +65,20 @@ struct BlurTile {
   static_assert(NWIN % 4 == 0 && LP % 8 == 4 && LP >= LW, "window layout");
 };
 
+// Next octave's plane 0 written by the blur of plane nOctaveLayers = 2
+// (src/sift.cpp:252-254, INTER_NEAREST at exactly half size: (y, x) <- (2y, 2x)),
+// so no decimation launch; p == nullptr: not fused.
+struct NextPlane {
+  float* p;
+  long long pitch;
+  int rows, cols;
+};
+
 template <int W>
 __device__ __forceinline__ void blur_tile(const float* __restrict__ src, long long spitch, int rows,
                                           int cols, float* __restrict__ dst, long long dpitch,
                                           const float* __restrict__ coef, int x0, int y0,
-                                          float* __restrict__ lds) {
+                                          float* __restrict__ lds, NextPlane nx = NextPlane{nullptr, 0, 0, 0}) {
   using T = BlurTile<W>;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int r = wv; r < T::LR; r += 4) {
@@ -131,6 +140,13 @@ __device__ __forceinline__ void blur_tile(const float* __restrict__ src, long lo
       for (int p = 0; p < kPX; ++p)
         if (x + p < cols) drow[p] = acc[p] / 8192.f;
     }
+    // x is even (kPX-aligned); even rows: outputs 0, 2, 4, 6 -> next plane (y/2, x/2 + q)
+    if (nx.p && (y & 1) == 0 && (y >> 1) < nx.rows) {
+      float* nrow = nx.p + (long long)(y >> 1) * nx.pitch + (x >> 1);
+#pragma unroll
+      for (int q = 0; q < kPX / 2; ++q)
+        if ((x >> 1) + q < nx.cols) nrow[q] = acc[2 * q] / 8192.f;
+    }
   }
 }
 
@@ -155,6 +171,7 @@ struct OctaveArgs {
   long long dst_off[4];
   const float* coef[4];
   int pitch, rows, cols, pad_;
+  NextPlane nx;  // fused decimation of plane 2 (scale index 1), or p == nullptr
 };
 
 // The four non-base scales of one octave (src/sift.cpp:256-258): each is
@@ -169,9 +186,11 @@ __global__ __launch_bounds__(256) void blur_octave_kernel(OctaveArgs A) {
   const float* src = A.gpyr + b * A.g_img + A.base_off;
   float* dst = A.gpyr + b * A.g_img + A.dst_off[si];
   const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTY;
+  NextPlane nx = A.nx;
+  if (nx.p) nx.p += b * A.g_img;
   switch (si) {
     case 0: blur_tile<4>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[0], x0, y0, lds); break;
-    case 1: blur_tile<8>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[1], x0, y0, lds); break;
+    case 1: blur_tile<8>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[1], x0, y0, lds, nx); break;
     case 2: blur_tile<12>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[2], x0, y0, lds); break;
     default: blur_tile<18>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[3], x0, y0, lds); break;
   }
@@ -231,8 +250,21 @@ void launch_blur_plane(hipStream_t st, int w, const float* coef, Plane src, floa
   }
 }
 
+// Octave o+1's plane 0 from this launch's plane 2 when it is an exact half
+// (the caller then skips the decimation); else not fused.
+static NextPlane next_plane(const Layout& L, int o, float* gpyr, bool fuse) {
+  if (!fuse || o + 1 >= L.n_oct || L.oct[o].rows != 2 * L.oct[o + 1].rows || L.oct[o].cols != 2 * L.oct[o + 1].cols)
+    return NextPlane{nullptr, 0, 0, 0};
+  const Octave& N = L.oct[o + 1];
+  return NextPlane{gpyr + N.g_off[0], N.pitch, N.rows, N.cols};
+}
+
+bool blur_fuses_decimation(const Layout& L, int o) {
+  return o > 0 && L.oct[o - 1].rows == 2 * L.oct[o].rows && L.oct[o - 1].cols == 2 * L.oct[o].cols;
+}
+
 void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
-                        const int* wsz, int batch) {
+                        const int* wsz, int batch, bool fuse_next) {
   const Octave& O = L.oct[o];
   OctaveArgs A;
   A.gpyr = gpyr;
@@ -248,6 +280,7 @@ void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, con
   A.rows = O.rows;
   A.cols = O.cols;
   A.pad_ = 0;
+  A.nx = next_plane(L, o, gpyr, fuse_next);
   dim3 grid((O.cols + kTileW - 1) / kTileW, (O.rows + kTY - 1) / kTY, batch * 4);
   hipLaunchKernelGGL(blur_octave_kernel, grid, dim3(256), lds_bytes_for(18), st, A);
 }
@@ -280,7 +313,8 @@ template <int W>
 __device__ __forceinline__ void blur_small_tile(const float* __restrict__ src, long long spitch, int rows, int cols,
                                                 float* __restrict__ dst, long long dpitch,
                                                 const float* __restrict__ coef, int x0, int y0,
-                                                float* __restrict__ lds) {
+                                                float* __restrict__ lds,
+                                                NextPlane nx = NextPlane{nullptr, 0, 0, 0}) {
   using T = SmallTile<W>;
   const int t = threadIdx.x;
   float* kt = lds + T::LR * kSLP;
@@ -329,6 +363,9 @@ __device__ __forceinline__ void blur_small_tile(const float* __restrict__ src, l
     float* drow = dst + (long long)y * dpitch + x;
     if (x < cols) drow[0] = acc0 / 8192.f;
     if (x + 1 < cols) drow[1] = acc1 / 8192.f;
+    // x is even: output 0 -> next plane (y/2, x/2) on even rows
+    if (nx.p && (y & 1) == 0 && (y >> 1) < nx.rows && (x >> 1) < nx.cols)
+      nx.p[(long long)(y >> 1) * nx.pitch + (x >> 1)] = acc0 / 8192.f;
   }
 }
 
@@ -341,9 +378,11 @@ __global__ __launch_bounds__(256) void blur_small_kernel(OctaveArgs A) {
   const float* src = A.gpyr + b * A.g_img + A.base_off;
   float* dst = A.gpyr + b * A.g_img + A.dst_off[si];
   const int x0 = blockIdx.x * kSW, y0 = blockIdx.y * kSH;
+  NextPlane nx = A.nx;
+  if (nx.p) nx.p += b * A.g_img;
   switch (si) {
     case 0: blur_small_tile<4>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[0], x0, y0, lds); break;
-    case 1: blur_small_tile<8>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[1], x0, y0, lds); break;
+    case 1: blur_small_tile<8>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[1], x0, y0, lds, nx); break;
     case 2: blur_small_tile<12>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[2], x0, y0, lds); break;
     default: blur_small_tile<18>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[3], x0, y0, lds); break;
   }
@@ -356,7 +395,7 @@ long long blur_octave_tiles(const Layout& L, int o, int batch) {
 }
 
 void launch_blur_octave_small(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
-                              const int* wsz, int batch) {
+                              const int* wsz, int batch, bool fuse_next) {
   const Octave& O = L.oct[o];
   OctaveArgs A;
   A.gpyr = gpyr;
@@ -372,6 +411,7 @@ void launch_blur_octave_small(hipStream_t st, const Layout& L, int o, float* gpy
   A.rows = O.rows;
   A.cols = O.cols;
   A.pad_ = 0;
+  A.nx = next_plane(L, o, gpyr, fuse_next);
   dim3 grid((O.cols + kSW - 1) / kSW, (O.rows + kSH - 1) / kSH, batch * 4);
   hipLaunchKernelGGL(blur_small_kernel, grid, dim3(256), SmallTile<18>::LDS_FLOATS * 4, st, A);
 }

@@ -205,12 +205,15 @@ struct Plane {          // a device plane (or the input image)
 // blur.hip
 void launch_blur_plane(hipStream_t st, int w, const float* coef, Plane src, float* dst,
                        long long dpitch, long long dimg, int rows, int cols, int batch);
+// fuse_next: also write octave o+1's plane 0 (the INTER_NEAREST half of plane
+// 2) when blur_fuses_decimation(L, o + 1); the caller then skips the decimation.
 void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
-                        const int* wsz, int batch);
+                        const int* wsz, int batch, bool fuse_next = false);
+bool blur_fuses_decimation(const Layout& L, int o);
 // The same planes for small launches (2 outputs per lane, 32 x 16 tiles;
 // round 3): picked when blur_octave_tiles(...) is below the context's limit.
 void launch_blur_octave_small(hipStream_t st, const Layout& L, int o, float* gpyr, const float* coefs,
-                              const int* wsz, int batch);
+                              const int* wsz, int batch, bool fuse_next = false);
 long long blur_octave_tiles(const Layout& L, int o, int batch);
 // Exact blur in symmetric scatter form for SIFT_NCL's five fixed tables
 // (compile-time constants); sym_tables_match(coefs) checks them against the

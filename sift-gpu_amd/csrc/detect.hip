@@ -631,9 +631,18 @@ __global__ __launch_bounds__(kScanT) void scan_down_kernel(const int* __restrict
 // candidate blocks and orientation peaks): one launch instead of three, on a
 // path whose launches are latency-bound.  Thread t owns the `per` consecutive
 // elements [t * per, t * per + per); out[n] = total.
+// Per-image offsets from a scan: gout[b] = out[b * stride] (idx == nullptr) or
+// out[min(idx[b], n)], b = 0..batch (gather_offsets_kernel's contract).
+struct ScanGather {
+  const int* idx;
+  int stride, batch;
+  int* gout;  // nullptr: no gather
+};
+
 constexpr int kScanSmallMax = 1024 * 64;  // one 1080p image: 64,800 candidates
 __global__ __launch_bounds__(1024) void scan_small_kernel(const int* __restrict__ in, const int* n_dev, int n_host,
-                                                          int cap, int* __restrict__ out, int* total_out) {
+                                                          int cap, int* __restrict__ out, int* total_out,
+                                                          ScanGather g) {
   __shared__ int wsum[16];
   const int n = scan_n(n_dev, n_host, cap);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -662,16 +671,40 @@ __global__ __launch_bounds__(1024) void scan_small_kernel(const int* __restrict_
     out[n] = tot;
     if (total_out) *total_out = tot;
   }
+  if (g.gout) {  // the gather of the per-image offsets, after the whole scan is written
+    __syncthreads();
+    for (int b = tid; b <= g.batch; b += 1024) {
+      int i = b * g.stride;
+      if (g.idx) i = g.idx[b] < n ? g.idx[b] : n;
+      g.gout[b] = out[i];
+    }
+  }
 }
 
 int scan_tiles_for(long long cap) { return (int)((cap + kScanTile - 1) / kScanTile); }
 
+__global__ void gather_offsets_kernel(const int* __restrict__ scan, const int* __restrict__ idx,
+                                      int stride, int batch, const int* n_dev, int cap,
+                                      int* __restrict__ out);
+
 void launch_scan(hipStream_t st, const int* in, int* out, const int* n_dev, int n_host, int cap, int* total_out,
-                 int* tsum) {
+                 int* tsum, ScanGather g = ScanGather{nullptr, 0, 0, nullptr}) {
   if (cap <= kScanSmallMax) {
-    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, in, n_dev, n_host, cap, out, total_out);
+    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(1024), 0, st, in, n_dev, n_host, cap, out, total_out, g);
     return;
   }
+  struct Tail {  // the three-kernel scan, then the gather as its own launch
+    hipStream_t st;
+    const int* out;
+    const int* n_dev;
+    int cap;
+    ScanGather g;
+    ~Tail() {
+      if (g.gout)
+        hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(256), 0, st, out, g.idx, g.stride, g.batch,
+                           g.idx ? n_dev : nullptr, cap, g.gout);
+    }
+  } tail{st, out, n_dev, cap, g};
   const int nt = scan_tiles_for(cap) > 0 ? scan_tiles_for(cap) : 1;
   hipLaunchKernelGGL(scan_reduce_kernel, dim3(nt), dim3(kScanT), 0, st, in, n_dev, n_host, cap, tsum);
   hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, st, tsum, nt, n_dev, n_host, cap, out, total_out);
@@ -788,9 +821,8 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
   hipLaunchKernelGGL(mask_count_kernel, dim3(M.bpw, batch), dim3(256), 0, st, D.mask, M.w_img, M.bpw,
                      D.blk_counts);
   const int nblk = M.bpw * batch;
-  launch_scan(st, D.blk_counts, D.scan_tmp, nullptr, nblk, nblk, D.cand_total, D.scan_tiles);
-  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(256), 0, st, D.scan_tmp, nullptr, M.bpw,
-                     batch, nullptr, 0, D.img_cand_off);
+  launch_scan(st, D.blk_counts, D.scan_tmp, nullptr, nblk, nblk, D.cand_total, D.scan_tiles,
+              ScanGather{nullptr, M.bpw, batch, D.img_cand_off});
   hipLaunchKernelGGL(mask_expand_kernel, dim3(M.bpw, batch), dim3(256), 0, st, M, D.mask, D.scan_tmp,
                      D.cands, D.cand_cap);
 }
@@ -1423,15 +1455,17 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.cand_cap = D.cand_cap;
   A.couts = D.couts;
   A.npeaks = D.npeaks;
-  (void)batch;
   hipLaunchKernelGGL(refine_kernel, dim3(resident_grid((const void*)refine_kernel, 256, 0, 2048)), dim3(256), 0, st, A);
-  // slots per lane group: 2 (default); SIFT_HIP_ORIENT_SLOTS=1 selects the
-  // one-candidate-per-group orient_kernel, 3 / 4 the wider variants (A/B runs)
-  static const int slots = [] {
+  // slots per lane group: 2 for batches; 1 (the one-candidate-per-group
+  // orient_kernel: twice the waves) for one image, whose launch leaves most
+  // SIMDs with one wave (round 3: 0.93 vs 0.95 ms per 1080p image);
+  // SIFT_HIP_ORIENT_SLOTS=1..4 forces a variant (A/B runs)
+  static const int slots_env = [] {
     const char* e = getenv("SIFT_HIP_ORIENT_SLOTS");
-    const int v = e ? atoi(e) : 2;
-    return v >= 1 && v <= 4 ? v : 2;
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 4 ? v : 0;
   }();
+  const int slots = slots_env ? slots_env : batch == 1 ? 1 : 2;
   if (slots == 1)
     hipLaunchKernelGGL(orient_kernel, dim3(resident_grid((const void*)orient_kernel, 64, 0, 8192)), dim3(64), 0, st,
                        A);
@@ -1502,9 +1536,8 @@ void launch_status(hipStream_t st, const int* cand_total, int cand_cap, const in
 void launch_emit(hipStream_t st, DetectBufs& D, int batch, sift_keypoint* kpts, int kp_cap,
                  int* img_kp_off) {
   // kp_scan = exclusive scan of npeaks over the (clamped) candidate list
-  launch_scan(st, D.npeaks, D.kp_scan, D.cand_total, 0, D.cand_cap, D.kp_total, D.scan_tiles);
-  hipLaunchKernelGGL(gather_offsets_kernel, dim3(1), dim3(256), 0, st, D.kp_scan, D.img_cand_off,
-                     0, batch, D.cand_total, D.cand_cap, img_kp_off);
+  launch_scan(st, D.npeaks, D.kp_scan, D.cand_total, 0, D.cand_cap, D.kp_total, D.scan_tiles,
+              ScanGather{D.img_cand_off, 0, batch, img_kp_off});
   hipLaunchKernelGGL(emit_kernel, dim3(1024), dim3(256), 0, st, D.couts, D.kp_scan, D.cand_total,
                      D.cand_cap, kpts, kp_cap);
 }
