@@ -30,6 +30,11 @@
 
 #include <type_traits>
 
+// waves per SIMD the batch descriptor kernel is compiled for (register budget)
+#ifndef DESC_WPE
+#define DESC_WPE 4
+#endif
+
 namespace sift {
 
 __device__ __forceinline__ void wave_sync_d() {
@@ -108,7 +113,7 @@ struct RecT<true> {
 // image, round 3): its gather is issued a step earlier, so a wave that is
 // alone on its SIMD does not wait a full memory latency per batch.
 template <bool PACKED, bool DET, int PF = 1>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF == 2 ? 2 : PACKED ? 4 : 1))) void
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF == 2 ? 2 : PACKED ? DESC_WPE : 1))) void
 descriptor_kernel(DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
   // per-sample hand-off records (see RecT)

@@ -425,29 +425,40 @@ __device__ __forceinline__ void tri_walk(const TriArgs& A, void* ldsv, int b, in
       hbuf = L.h;
       brow = &L.base[slot][lane >> 4][4 * (lane & 15)];
     }
-    // ---- row pass of the role's scales (lane = row, 4 columns; rows
-    // lane >> 4 + r4) into the wave's own h rows, read back as lane = column ----
-#pragma unroll
-    for (int r4 = 0; r4 < kTB; r4 += 4) {
-      float h1[4], h2[4];
-      pt_rows<W1, W2>(brow + r4 * kTPit, h1, h2);
-      const int j = (lane >> 4) + r4, i = lane & 15;
-      *reinterpret_cast<float4*>(&hbuf[R_::h1][j][4 * i]) = make_float4(h1[0], h1[1], h1[2], h1[3]);
-      if constexpr (W2 != 0)
-        *reinterpret_cast<float4*>(&hbuf[R_::h2][j][4 * i]) = make_float4(h2[0], h2[1], h2[2], h2[3]);
-    }
-    pt_wave_sync();
-    float c1[kTB], c2[kTB];
-#pragma unroll
-    for (int j = 0; j < kTB; ++j) {
-      c1[j] = hbuf[R_::h1][j][lane];
-      if constexpr (W2 != 0) c2[j] = hbuf[R_::h2][j][lane];
-    }
-    pt_wave_sync();
-    // ---- column pass: lane = column; phase M of the role's slot cycle ----
+    // The step's source rows [Ys, Ys + kTB) reach outputs [Ys - W1, Ys + kTB - 1 + W1]
+    // only; a step whose rows reach no output of [y0, y1) (the lead and tail
+    // rows beyond this role's width, and octave 0's prologue) skips both
+    // passes: its stores drop anyway and the accumulators it would touch are
+    // assigned afresh before any stored output uses them.
+    const bool live = Ys + kTB - 1 + W1 >= y0 && Ys - W1 < y1;
     float o1[kTB], o2[kTB];
-    pt_col<W1, P1, M>(a1, c1, o1, std::make_integer_sequence<int, kTB>{});
-    if constexpr (W2 != 0) pt_col<W2, P2, M>(a2, c2, o2, std::make_integer_sequence<int, kTB>{});
+    if (live) {
+      // ---- row pass of the role's scales (lane = row, 4 columns; rows
+      // lane >> 4 + r4) into the wave's own h rows, read back as lane = column ----
+#pragma unroll
+      for (int r4 = 0; r4 < kTB; r4 += 4) {
+        float h1[4], h2[4];
+        pt_rows<W1, W2>(brow + r4 * kTPit, h1, h2);
+        const int j = (lane >> 4) + r4, i = lane & 15;
+        *reinterpret_cast<float4*>(&hbuf[R_::h1][j][4 * i]) = make_float4(h1[0], h1[1], h1[2], h1[3]);
+        if constexpr (W2 != 0)
+          *reinterpret_cast<float4*>(&hbuf[R_::h2][j][4 * i]) = make_float4(h2[0], h2[1], h2[2], h2[3]);
+      }
+      pt_wave_sync();
+      float c1[kTB], c2[kTB];
+#pragma unroll
+      for (int j = 0; j < kTB; ++j) {
+        c1[j] = hbuf[R_::h1][j][lane];
+        if constexpr (W2 != 0) c2[j] = hbuf[R_::h2][j][lane];
+      }
+      pt_wave_sync();
+      // ---- column pass: lane = column; phase M of the role's slot cycle ----
+      pt_col<W1, P1, M>(a1, c1, o1, std::make_integer_sequence<int, kTB>{});
+      if constexpr (W2 != 0) pt_col<W2, P2, M>(a2, c2, o2, std::make_integer_sequence<int, kTB>{});
+    } else {
+#pragma unroll
+      for (int j = 0; j < kTB; ++j) o1[j] = o2[j] = 0.f;
+    }
     // ---- stores: the step's completed outputs ----
 #pragma unroll
     for (int j = 0; j < kTB; ++j) {
