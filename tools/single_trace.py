@@ -39,7 +39,10 @@ def main():
             ctx.sync()
             if i >= 3:
                 ts.append(time.perf_counter() - t0)
-        print(f'{{"latency_ms": {np.median(ts) * 1e3:.4f}, "keypoints": {int(offs[1].item())}}}', flush=True)
+        n = int(offs[1].item())
+        h = int(desc[:n].contiguous().view(torch.int32).to(torch.int64).mul_(
+            torch.arange(1, n * 128 + 1, device="cuda", dtype=torch.int64).view(n, 128)).sum().item())
+        print(f'{{"latency_ms": {np.median(ts) * 1e3:.4f}, "keypoints": {n}, "desc_hash": {h}}}', flush=True)
 
 
 if __name__ == "__main__":
