@@ -1042,6 +1042,10 @@ __device__ __forceinline__ int ori_radius(float size, int o) {
 #ifndef ORIENT1_GRID
 #define ORIENT1_GRID 8192
 #endif
+// orient_kernel: gathers one step ahead (1) or at the step (0)
+#ifndef ORIENT_PF
+#define ORIENT_PF 0
+#endif
 #ifndef ORIENT_DPP
 #define ORIENT_DPP 0
 #endif
@@ -1129,11 +1133,15 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
       ++si;
     }
     // kOU batches of 8 samples per step: the kOU gathers are issued together
-    // (branch-free, clamped address), then the adds run in sample order
-    for (int base = 0; base < nmax; base += 8 * kOU) {
+    // (branch-free, clamped address), then the adds run in sample order.
+    // ORIENT_PF: the next step's gathers are issued before this step's adds,
+    // so a wave alone on its SIMD does not wait a memory latency per step.
+    struct Step {
       float2 mo[kOU];
       int ii[kOU], jv[kOU];
       bool okv[kOU];
+    };
+    auto fetch = [&](int base, Step& S) {
 #pragma unroll
       for (int u = 0; u < kOU; ++u) {
         const int i = si - radius, j = sj - radius;
@@ -1143,11 +1151,27 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
           ++si;
         }
         const int y = rr + i, x = rc + j;
-        okv[u] = base + 8 * u + q < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
-        ii[u] = i;
-        jv[u] = j;
-        mo[u] = gimg[okv[u] ? (long long)y * pitch + x : 0];  // (Mag, Ori) of the pixel
+        S.okv[u] = base + 8 * u + q < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
+        S.ii[u] = i;
+        S.jv[u] = j;
+        S.mo[u] = gimg[S.okv[u] ? (long long)y * pitch + x : 0];  // (Mag, Ori) of the pixel
       }
+    };
+#if ORIENT_PF
+    Step nxt;
+    if (nmax > 0) fetch(0, nxt);
+#endif
+    for (int base = 0; base < nmax; base += 8 * kOU) {
+#if ORIENT_PF
+      const Step cur = nxt;
+      fetch(base + 8 * kOU, nxt);  // branch-free: past the window it gathers the clamped address
+#else
+      Step cur;
+      fetch(base, cur);
+#endif
+      const float2* mo = cur.mo;
+      const int *ii = cur.ii, *jv = cur.jv;
+      const bool* okv = cur.okv;
 #pragma unroll
       for (int u = 0; u < kOU; ++u) {
         const float w = exp32f((ii[u] * ii[u] + jv[u] * jv[u]) * escale, etab, ek);
