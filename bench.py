@@ -739,14 +739,7 @@ def exact_block(a, world, B, R, C, S, res, tr):
 
 
 def fast_kernel():
-    """The SIFT_FLAG_FAST pyramid the library selects (sift-gpu_amd/csrc/api.hip,
-    read at context creation): pyramid_tri.hip unless a switch names another."""
-    def on(k):
-        return os.environ.get(k, "0") not in ("", "0")
-    if on("SIFT_HIP_FAST_V1"):
-        return "pyr_fast_kernel", "pyramid_fast.hip"
-    if on("SIFT_HIP_FAST_PAIR"):
-        return "pyr_pair_kernel", "pyramid_pair.hip"
+    """The SIFT_FLAG_FAST pyramid kernel (sift-gpu_amd/csrc/pyramid_tri.hip)."""
     return "pyr_tri_kernel", "pyramid_tri.hip"
 
 

@@ -42,6 +42,7 @@ def lib():
         L.so_gaussian_blur_1d.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_double, fp]
         L.so_resize_nn.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, ctypes.c_int, ctypes.c_int]
         L.so_build_gaussian_pyramid.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp]
+        L.so_fast_pyramid.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp]
         L.so_build_dog_pyramid.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp]
         L.so_pyramid_offsets.restype = ctypes.c_size_t
         L.so_pyramid_offsets.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -135,6 +136,16 @@ def build_gaussian_pyramid(img: np.ndarray, n_octaves: int = 5) -> np.ndarray:
     r, c = img.shape
     out = np.empty(_plane_total(r, c, n_octaves, 5), np.float32)
     lib().so_build_gaussian_pyramid(_fp(img), r, c, n_octaves, _fp(out))
+    return out
+
+
+def fast_pyramid(img: np.ndarray, n_octaves: int = 5) -> np.ndarray:
+    """The library's SIFT_FLAG_FAST separable pyramid in its exact operation
+    order (agreement mode, not the reference's arithmetic), packed."""
+    img = np.ascontiguousarray(img, np.float32)
+    r, c = img.shape
+    out = np.empty(_plane_total(r, c, n_octaves, 5), np.float32)
+    lib().so_fast_pyramid(_fp(img), r, c, n_octaves, _fp(out))
     return out
 
 

@@ -285,6 +285,86 @@ void so_build_gaussian_pyramid(const float* img, int rows, int cols, int n_octav
     }
 }
 
+/* ---- SIFT_FLAG_FAST pyramid (the library's separable form) -------------
+ * Not the reference's arithmetic: the separable agreement mode of
+ * sift-gpu_amd/csrc/pyramid_tri.hip, restated here so that its planes can be
+ * checked bit for bit.  Taps g(a) = (float)(exp(-a^2 / den) / sqrt(2 pi s^2))
+ * with den = (double)(2 s s) in float (the square root of getGaussianKernel's
+ * normalisation, src/sift.cpp:97-107).  Every blur reads its source with zero
+ * padding outside [0, rows-1) x [0, cols-1) (src/sift.cpp:116).
+ *   row pass:            h = g0 x[c]; h = fmaf(g_k, x[c-k] + x[c+k], h), k = 1..w
+ *   base column pass:    the same folded form down the column
+ *   scale column pass:   o = g_w h[r-w]; o = fmaf(g_|d|, h[r+d], o), d = -w+1..w
+ * Octave 0's plane 0 is the base blur (w = 4) of the image; plane 0 of octave
+ * o > 0 is resize INTER_NEAREST of plane 2 of octave o-1 (src/sift.cpp:252). */
+static int fast_taps(float sigma, float* g) {
+  const int w = (int)floor(3 * sigma);
+  const double den = (double)(2 * sigma * sigma);
+  const double nrm = 1. / sqrt(2 * K_PI * sigma * sigma);
+  for (int a = -w; a <= w; ++a) g[a + w] = (float)(nrm * exp(-(a * a) * 1. / den));
+  return w;
+}
+
+static float fast_src(const float* p, int rows, int cols, int r, int c) {
+  return (r >= 0 && r < rows - 1 && c >= 0 && c < cols - 1) ? p[(size_t)r * cols + c] : 0.f;
+}
+
+static void fast_blur(const float* src, int rows, int cols, float sigma, int folded_cols, float* dst) {
+  float gt[64];
+  const int w = fast_taps(sigma, gt);
+  const float* g = gt + w; /* g[a], a in [-w, w] */
+  float* h = (float*)malloc(sizeof(float) * (size_t)(rows + 2 * w) * cols);
+  /* row pass for rows [-w, rows + w): zero rows outside give h = +0 */
+#pragma omp parallel for schedule(static)
+  for (int r = -w; r < rows + w; ++r)
+    for (int c = 0; c < cols; ++c) {
+      float v = g[0] * fast_src(src, rows, cols, r, c);
+      for (int k = 1; k <= w; ++k)
+        v = fmaf(g[k], fast_src(src, rows, cols, r, c - k) + fast_src(src, rows, cols, r, c + k), v);
+      h[(size_t)(r + w) * cols + c] = v;
+    }
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c) {
+#define HH(rr) h[(size_t)((rr) + w) * cols + c]
+      float o;
+      if (folded_cols) {
+        o = g[0] * HH(r);
+        for (int k = 1; k <= w; ++k) o = fmaf(g[k], HH(r - k) + HH(r + k), o);
+      } else {
+        o = g[w] * HH(r - w);
+        for (int d = -w + 1; d <= w; ++d) o = fmaf(g[d < 0 ? -d : d], HH(r + d), o);
+      }
+#undef HH
+      dst[(size_t)r * cols + c] = o;
+    }
+  free(h);
+}
+
+void so_fast_pyramid(const float* img, int rows, int cols, int n_octaves, float* gpyr) {
+  size_t off[32 * 5];
+  int orow[32], ocol[32];
+  so_pyramid_offsets(rows, cols, n_octaves, N_SCALES, off);
+  so_octave_shapes(rows, cols, n_octaves, orow, ocol);
+  float sig[N_SCALES];
+  double k = pow(2.0, 1.0 / N_LAYERS);
+  sig[0] = (float)sqrt(K_SIGMA * K_SIGMA + 0.2 * 0.2);
+  for (int i = 1; i < N_SCALES; ++i) {
+    double tot = pow(k * 1.0, (double)i) * K_SIGMA;
+    sig[i] = (float)sqrt(tot * tot - K_SIGMA * K_SIGMA);
+  }
+  for (int o = 0; o < n_octaves; ++o)
+    for (int s = 0; s < N_SCALES; ++s) {
+      float* dst = gpyr + off[o * N_SCALES + s];
+      if (o == 0 && s == 0)
+        fast_blur(img, rows, cols, sig[0], 1, dst);
+      else if (s == 0)
+        so_resize_nn(gpyr + off[(o - 1) * N_SCALES + N_LAYERS], orow[o - 1], ocol[o - 1], dst, orow[o], ocol[o]);
+      else
+        fast_blur(gpyr + off[o * N_SCALES], orow[o], ocol[o], sig[s], 0, dst);
+    }
+}
+
 /* ---- buildDoGPyramid (src/sift.cpp:265-283) ---------------------------- */
 void so_build_dog_pyramid(const float* gpyr, int rows, int cols, int n_octaves, float* dog) {
   size_t goff[32 * 5], doff[32 * 4];

@@ -66,6 +66,11 @@ void so_resize_nn(const float* src, int srows, int scols, float* dst, int drows,
  * octave, correct o*5+s indexing -- identical to the reference at 5). */
 void so_build_gaussian_pyramid(const float* img, int rows, int cols, int n_octaves, float* gpyr);
 
+/* The library's SIFT_FLAG_FAST separable pyramid (agreement mode, not the
+ * reference's arithmetic), in its exact operation order; packed like
+ * so_build_gaussian_pyramid. */
+void so_fast_pyramid(const float* img, int rows, int cols, int n_octaves, float* gpyr);
+
 /* buildDoGPyramid (src/sift.cpp:265-283), packed output (4 planes/octave). */
 void so_build_dog_pyramid(const float* gpyr, int rows, int cols, int n_octaves, float* dog);
 

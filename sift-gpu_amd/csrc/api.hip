@@ -132,9 +132,7 @@ struct sift_ctx {
   long long gpyr_elems = 0, dog_elems = 0;
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
-  std::vector<char> fast_taps;    // SIFT_FLAG_FAST 1-D taps (pyramid_fast.hip), passed by value
-  bool fast_pair = true;          // SIFT_FLAG_FAST via pyramid_pair.hip / pyramid_tri.hip (round 3)
-  bool fast_tri = true;           // pyramid_tri.hip (SIFT_HIP_FAST_PAIR=1: pyramid_pair.hip)
+  bool fast_ok = false;           // SIFT_FLAG_FAST: pyramid_tri.hip's compiled-in taps equal the host's
   bool fuse_dec = true;           // 2-D tile blurs write the next plane 0 (SIFT_HIP_FUSE_DEC=0: decimate_kernel)
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
@@ -260,6 +258,20 @@ int check_dims(sift_ctx* c, int rows, int cols, int n_oct, int batch) {
   return SIFT_OK;
 }
 
+// SIFT_FLAG_FAST preconditions: pyramid_tri.hip's literal taps equal the host
+// formula, and every plane and the input rows stay below the buffer offset
+// its dropped loads and stores use (without the size check a plane
+// of ~530 M pixels would read real pixels as padding and write inside itself).
+int check_fast(sift_ctx* c, const Layout& L, long long src_row_stride) {
+  if (!(c->flags & SIFT_FLAG_FAST)) return SIFT_OK;
+  if (!c->fast_ok) return fail(c, SIFT_E_INVALID, "SIFT_FLAG_FAST: compiled-in separable taps differ from the host's");
+  if (!pyramid_tri_fits(L, src_row_stride))
+    return fail(c, SIFT_E_SIZE,
+                "SIFT_FLAG_FAST: the octave-0 plane or the input rows exceed the separable pyramid's "
+                "2,130,706,432-byte buffer-offset range");
+  return SIFT_OK;
+}
+
 // coefficient scratch for arbitrary sigma
 int ensure_coef_gen(sift_ctx* c, size_t n) {
   if (n <= c->coef_gen_cap) return SIFT_OK;
@@ -323,24 +335,16 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
     for (int o = 0; o < L.n_oct; ++o) {
       const double px = plane_px(L, o) * batch;
       const double taps = 2.0 * (9 + 17 + 25 + 37) + (o == 0 ? 2.0 * 9 : 0.0);
-      if (c->fast_pair) {
-        // pyramid_pair.hip: octave o-1's launch wrote plane 0 of octave o when
-        // it is an exact half; otherwise decimate first (plane 0
-        // is one of the five plane writes, the decimation's read is not
-        // algorithmic, so it is outside the pyramid stage's bytes)
-        if (o > 0 && !pyramid_pair_fuses(L, o)) {
-          StageScope s(c, ST_DECIMATE, 0, 8.0 * px);
-          launch_decimate(st, L, o, c->d_gpyr, batch);
-        }
-        StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-        if (c->fast_tri)
-          launch_pyramid_tri(st, L, o, c->d_gpyr, src, batch);
-        else
-          launch_pyramid_pair(st, L, o, c->d_gpyr, src, batch);
-      } else {
-        StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-        launch_pyramid_fast(st, L, o, c->d_gpyr, src, batch, c->fast_taps.data());
+      // pyramid_tri.hip: octave o-1's launch wrote plane 0 of octave o when
+      // it is an exact half; otherwise decimate first (plane 0
+      // is one of the five plane writes, the decimation's read is not
+      // algorithmic, so it is outside the pyramid stage's bytes)
+      if (o > 0 && !pyramid_fuses_decimation(L, o)) {
+        StageScope s(c, ST_DECIMATE, 0, 8.0 * px);
+        launch_decimate(st, L, o, c->d_gpyr, batch);
       }
+      StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
+      launch_pyramid_tri(st, L, o, c->d_gpyr, src, batch);
     }
     if (with_dog)
       for (int o = 0; o < L.n_oct; ++o) {
@@ -697,15 +701,10 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     const char* sm = getenv("SIFT_HIP_SMALL_MAX");
     if (sm) c->small_max = atoll(sm);
   }
-  c->fast_taps.resize(fast_coefs_size());
-  if (fast_coefs_host(sb, sig_f, c->fast_taps.data()) != 0) return bail(SIFT_E_INVALID);
+  // SIFT_FLAG_FAST: pyramid_tri.hip carries its 1-D taps as literals; a
+  // mismatch with the host formula makes the flag an error (enqueue-time check)
+  c->fast_ok = fast_taps_match(sb, sig_f);
   {
-    // SIFT_FLAG_FAST: the wave-pair pyramid (literal taps, checked against the
-    // host's) unless SIFT_HIP_FAST_V1=1 selects round 2's pyr_fast_kernel
-    const char* e = getenv("SIFT_HIP_FAST_V1");
-    c->fast_pair = pair_taps_match(c->fast_taps.data()) && !(e && atoi(e) != 0);
-    const char* ep = getenv("SIFT_HIP_FAST_PAIR");
-    c->fast_tri = !(ep && atoi(ep) != 0);
     const char* fd = getenv("SIFT_HIP_FUSE_DEC");
     c->fuse_dec = !(fd && atoi(fd) == 0);
   }
@@ -849,6 +848,7 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
                 size_t img_stride, sift_keypoint* d_kpts, float* d_desc, int kp_cap, int* d_img_offsets) {
   const Layout L = make_layout(rows, cols, c->n_oct);
   const Plane src{d_imgs, (long long)row_stride, (long long)img_stride};
+  if (int rc = check_fast(c, L, (long long)row_stride)) return rc;
   if (c->flags & SIFT_FLAG_VERBOSE) {
     hipEvent_t v0 = get_event(c), v1 = get_event(c), v2 = get_event(c), v3 = get_event(c);
     (void)hipEventRecord(v0, c->stream);
@@ -1018,6 +1018,7 @@ int sift_build_gaussian_pyramid(sift_ctx* c, const float* img, int rows, int col
   if (rc) return rc;
   (void)hipSetDevice(c->device);
   const Layout L = make_layout(rows, cols, n_octaves);
+  if ((rc = check_fast(c, L, c->in_pitch))) return rc;
   if ((rc = upload_image(c, img, rows, cols, (size_t)cols * sizeof(float)))) return rc;
   enqueue_pyramid(c, L, Plane{c->d_in, c->in_pitch, c->in_img}, 1, false);
   HIP_TRY(c, hipGetLastError());

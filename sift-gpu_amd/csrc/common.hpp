@@ -229,12 +229,6 @@ void launch_blur_1d(hipStream_t st, int w, const float* coef1d, Plane src, float
 void launch_synth(hipStream_t st, float* out, int batch, int rows, int cols, long long pitch,
                   long long img_stride, int seed_base);
 
-// pyramid_fast.hip (SIFT_FLAG_FAST): separable row/column pyramid, one launch
-// per octave writing its five planes.  Coefficient block built on the host:
-// fast_coefs_host(base sigma, sig[1..4], out[fast_coefs_size()]) != 0 if the
-// kernel widths are not the unrolled 4 / 4, 8, 12, 18.
-size_t fast_coefs_size();
-int fast_coefs_host(float sigma_base, const float* sig, void* out);
 void launch_bgr8_gray(hipStream_t st, const uint8_t* src, long long sstride, long long simg, int srows, int scols,
                       float* dst, long long dpitch, long long dimg, int drows, int dcols, int batch);
 int find_homography_ransac(const float* src_xy, const float* dst_xy, int n, double thr, int max_iters,
@@ -243,17 +237,15 @@ void perspective_transform(const double* H, const float* xy, int n, float* out);
 int knn_splits(int nq, int nt);
 void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int nt, int k, int splits,
                    float2* part_d, int2* part_i, int* idx, float* dist);
-void launch_pyramid_fast(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch,
-                         const void* coef);
-// pyramid_pair.hip (SIFT_FLAG_FAST, round 3): octave o's five planes; octave
-// o+1's plane 0 too when pyramid_pair_fuses(L, o + 1) (else decimate first).
-// pair_taps_match(FastCoefs block): the compile-time taps equal the host's.
-void launch_pyramid_pair(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
-bool pyramid_pair_fuses(const Layout& L, int o);
-bool pair_taps_match(const void* coef);
-// pyramid_tri.hip (SIFT_FLAG_FAST, round 3, default): the same planes as
-// launch_pyramid_pair, three wave roles per workgroup.
+// pyramid_tri.hip (SIFT_FLAG_FAST): octave o's five planes by the separable
+// form, plus octave o+1's plane 0 when pyramid_fuses_decimation(L, o + 1)
+// (else decimate first).  fast_taps_match: the compiled-in 1-D taps equal
+// fast_taps_host's for these sigmas; pyramid_tri_fits: every plane and the
+// input rows below the kernel's dropped-offset range.
 void launch_pyramid_tri(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
+bool pyramid_fuses_decimation(const Layout& L, int o);
+bool fast_taps_match(float sigma_base, const float* sig);
+bool pyramid_tri_fits(const Layout& L, long long src_row_stride);
 
 // detect.hip
 struct DetectBufs {

@@ -1035,36 +1035,12 @@ __device__ __forceinline__ int ori_radius(float size, int o) {
   return cv_round(3 * 1.5f * scl);
 }
 
-// orient_kernel's histogram chain through DPP broadcasts (1) or lane-serial
-// LDS read-modify-writes (0, default: the same bits and the same time at one
-// image, profiles/r3_orient_chain_ab.txt)
-// workgroups of the one-image orient_kernel launch (upper bound)
-#ifndef ORIENT1_GRID
-#define ORIENT1_GRID 8192
-#endif
-// orient_kernel: gathers one step ahead (1) or at the step (0)
-#ifndef ORIENT_PF
-#define ORIENT_PF 0
-#endif
-#ifndef ORIENT_DPP
-#define ORIENT_DPP 0
-#endif
-// lane J of x's 8-lane group, for every lane (row_newbcast: lane n of each
-// 16-lane row; hi8 = lane & 8 picks the row's upper group)
-template <int J>
-__device__ __forceinline__ int bcast8(int x, bool hi8) {
-  const int lo = __builtin_amdgcn_update_dpp(0, x, 0x150 + J, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, x, 0x158 + J, 0xf, 0xf, false);
-  return hi8 ? hi : lo;
-}
-
 __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
   __shared__ float oh[kOGrp][kOriBins + 4];
   __shared__ float sm[kOGrp][kOriBins + 4];
   __shared__ int sord[kOGrp];
   const int lane = threadIdx.x & 63;
   const int g = lane >> 3, q = lane & 7;
-  const bool hi8 = (lane & 8) != 0;
   int n = *A.cand_total;
   if (n > A.cand_cap) n = A.cand_cap;
   const ExpConsts ek = A.mc->e;
@@ -1134,14 +1110,10 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
     }
     // kOU batches of 8 samples per step: the kOU gathers are issued together
     // (branch-free, clamped address), then the adds run in sample order.
-    // ORIENT_PF: the next step's gathers are issued before this step's adds,
-    // so a wave alone on its SIMD does not wait a memory latency per step.
-    struct Step {
+    for (int base = 0; base < nmax; base += 8 * kOU) {
       float2 mo[kOU];
       int ii[kOU], jv[kOU];
       bool okv[kOU];
-    };
-    auto fetch = [&](int base, Step& S) {
 #pragma unroll
       for (int u = 0; u < kOU; ++u) {
         const int i = si - radius, j = sj - radius;
@@ -1151,27 +1123,11 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
           ++si;
         }
         const int y = rr + i, x = rc + j;
-        S.okv[u] = base + 8 * u + q < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
-        S.ii[u] = i;
-        S.jv[u] = j;
-        S.mo[u] = gimg[S.okv[u] ? (long long)y * pitch + x : 0];  // (Mag, Ori) of the pixel
+        okv[u] = base + 8 * u + q < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
+        ii[u] = i;
+        jv[u] = j;
+        mo[u] = gimg[okv[u] ? (long long)y * pitch + x : 0];  // (Mag, Ori) of the pixel
       }
-    };
-#if ORIENT_PF
-    Step nxt;
-    if (nmax > 0) fetch(0, nxt);
-#endif
-    for (int base = 0; base < nmax; base += 8 * kOU) {
-#if ORIENT_PF
-      const Step cur = nxt;
-      fetch(base + 8 * kOU, nxt);  // branch-free: past the window it gathers the clamped address
-#else
-      Step cur;
-      fetch(base, cur);
-#endif
-      const float2* mo = cur.mo;
-      const int *ii = cur.ii, *jv = cur.jv;
-      const bool* okv = cur.okv;
 #pragma unroll
       for (int u = 0; u < kOU; ++u) {
         const float w = exp32f((ii[u] * ii[u] + jv[u] * jv[u]) * escale, etab, ek);
@@ -1179,37 +1135,23 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
         if (bin >= kOriBins) bin -= kOriBins;
         if (bin < 0) bin += kOriBins;
         const float val = w * mo[u].x;
-#if ORIENT_DPP
-        // The group's 8 samples in sample order without 8 LDS round trips:
-        // every lane reads its bin once, then step jj broadcasts lane jj's
-        // running sum (row_newbcast, DPP) to the later lanes of its group that
-        // share the bin, and only the last lane of each bin writes.  Every
-        // bin receives the same adds in the same order; an invalid sample
-        // adds +0.0 to bin 0 (exact no-op: every bin is >= +0).
-        const int bn = okv[u] ? bin : 0;
-        const float vl = okv[u] ? val : 0.f;
-        float c = oh[g][bn];
-        bool last = true;
-#define ORIENT_STEP(J)                                                      \
-  {                                                                         \
-    const int bj = bcast8<J>(bn, hi8);                                      \
-    const int vj = bcast8<J>(__float_as_int(c + vl), hi8);                  \
-    c = (q > J && bn == bj) ? __int_as_float(vj) : c;                       \
-    last = last && !(J > q && bn == bj);                                    \
-  }
-        ORIENT_STEP(0) ORIENT_STEP(1) ORIENT_STEP(2) ORIENT_STEP(3)
-        ORIENT_STEP(4) ORIENT_STEP(5) ORIENT_STEP(6) ORIENT_STEP(7)
-#undef ORIENT_STEP
-        if (last) oh[g][bn] = c + vl;
-#else
         // step jj: lane jj of every group adds its sample into its group's
         // histogram -- a plain read-modify-write (one lane per group, groups
         // own disjoint rows; the wave's LDS operations stay in program order,
-        // so step jj + 1 reads what step jj wrote)
+        // so step jj + 1 reads what step jj wrote).  As in orient_slots_kernel,
+        // each step tests a fresh opaque copy of q behind a compiler barrier:
+        // eight plain `q == jj` blocks are mutually exclusive for one thread,
+        // and hipcc once rebuilt them as a switch and ran the steps out of
+        // order (tools/check_orient_isa.py checks the compiled steps).
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj)
-          if (q == jj && okv[u]) oh[g][bin] = oh[g][bin] + val;
-#endif
+        for (int jj = 0; jj < 8; ++jj) {
+          int qv = q;
+          asm volatile("; orient step %1" : "+v"(qv) : "n"(jj) : "memory");
+          if (qv == jj && okv[u]) {
+            const float h = oh[g][bin];
+            oh[g][bin] = h + val;
+          }
+        }
       }
     }
     wave_sync();
@@ -1535,9 +1477,8 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   }();
   const int slots = slots_env ? slots_env : batch == 1 ? 1 : 2;
   if (slots == 1)
-    hipLaunchKernelGGL(orient_kernel,
-                       dim3(std::min(resident_grid((const void*)orient_kernel, 64, 0, 8192), ORIENT1_GRID)), dim3(64),
-                       0, st, A);
+    hipLaunchKernelGGL(orient_kernel, dim3(resident_grid((const void*)orient_kernel, 64, 0, 8192)), dim3(64), 0, st,
+                       A);
   else if (slots == 3)
     hipLaunchKernelGGL(orient_slots_kernel<3>,
                        dim3(resident_grid((const void*)orient_slots_kernel<3>, 64, 0, 8192)), dim3(64), 0, st, A);

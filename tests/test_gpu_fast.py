@@ -1,14 +1,16 @@
 """GPU tests of SIFT_FLAG_FAST: the separable row/column Gaussian pyramid
-(sift-gpu_amd/csrc/pyramid_tri.hip; pyramid_pair.hip and pyramid_fast.hip
-behind switches) in front of the exact downstream kernels.
+(sift-gpu_amd/csrc/pyramid_tri.hip) in front of the exact downstream kernels.
 
 Fast mode is NOT bit-exact with the reference's 2-D float chain
 (src/sift.cpp:137-146): it applies K[a][b] = 8192 g(a) g(b) as a row pass and
 a column pass with fused multiply-adds, so the pyramid differs from the CPU
-path by float rounding only.  These tests bound that difference against the
-CPU oracle:
-  * every Gaussian plane within an absolute tolerance (values are 0..255);
-  * the full SIFT_NCL output matched keypoint by keypoint against the
+path by float rounding only.  These tests
+  * pin the kernel to its own specification: every plane equals
+    oracle.fast_pyramid (oracle/sift_oracle.c so_fast_pyramid, the separable
+    form in its exact operation order) bit for bit;
+  * bound the difference to the reference's arithmetic: every Gaussian plane
+    within an absolute tolerance of the exact CPU path (values are 0..255);
+  * match the full SIFT_NCL output keypoint by keypoint against the
     north_star tolerance -- (x, y, size, angle) within 1e-3 and descriptor L2
     within 1e-4 -- with the match rates asserted (a rounding difference can
     flip a discrete decision: a DoG threshold, a cvRound step, an orientation
@@ -25,6 +27,8 @@ FAST = 0x1
 PLANE_ATOL = 2e-3      # |fast - exact| on 0..255 planes
 KP_TOL = 1e-3          # north_star: keypoint (x, y, sigma, theta) within 1e-3
 DESC_TOL = 1e-4        # north_star: descriptor L2 within 1e-4
+SHAPES = [((1080, 1920), 0), ((203, 157), 2), ((33, 1200), 12), ((300, 210), 3), ((130, 90), 6),
+          ((540, 960), 5), ((257, 4100), 7)]
 
 
 @pytest.fixture(scope="module")
@@ -34,55 +38,37 @@ def fctx(siftgpu):
     c.close()
 
 
-def _fast_ctx(siftgpu, kind, rows=1080, cols=1920, batch=4):
-    """A SIFT_FLAG_FAST context on one of the three separable pyramids:
-    pyramid_tri.hip (default, round 3), pyramid_pair.hip (SIFT_HIP_FAST_PAIR=1)
-    and round 2's pyramid_fast.hip (SIFT_HIP_FAST_V1=1); the switches are read
-    at context creation."""
-    import os
-    env = {"tri": {}, "pair": {"SIFT_HIP_FAST_PAIR": "1"}, "v1": {"SIFT_HIP_FAST_V1": "1"}}[kind]
-    keys = ("SIFT_HIP_FAST_PAIR", "SIFT_HIP_FAST_V1")
-    old = {k: os.environ.pop(k, None) for k in keys}
-    os.environ.update(env)
-    try:
-        return siftgpu.Context(rows, cols, batch, device=0, flags=FAST)
-    finally:
-        for k in keys:
-            os.environ.pop(k, None)
-            if old[k] is not None:
-                os.environ[k] = old[k]
-
-
-@pytest.fixture(scope="module", params=["tri", "pair", "v1"])
-def fctx_both(request, siftgpu):
-    c = _fast_ctx(siftgpu, request.param)
-    yield c
-    c.close()
-
-
-@pytest.mark.parametrize("shape,b", [((1080, 1920), 0), ((203, 157), 2), ((33, 1200), 12), ((540, 960), 5)])
-def test_fast_tri_equals_pair(siftgpu, oracle, shape, b):
-    """pyramid_tri.hip and pyramid_pair.hip apply the same row-pass chains and the
-    same in-order column scatter, so their planes are bit-identical."""
+@pytest.mark.parametrize("shape,b", SHAPES + [((4320, 7680), 1)])
+def test_fast_pyramid_equals_its_oracle(siftgpu, oracle, shape, b):
+    """Every plane of pyr_tri_kernel == so_fast_pyramid, bit for bit (the
+    base blur one step ahead of the scales, chunk seams, strip edges, odd
+    shapes, a 4100-column strip count, the 8K image)."""
     img = oracle.synth_image(b, *shape)
-    t = _fast_ctx(siftgpu, "tri", *shape, 1)
-    p = _fast_ctx(siftgpu, "pair", *shape, 1)
+    ctx = siftgpu.Context(*shape, 1, device=0, flags=FAST)
     try:
-        gt = t.buildGaussianPyramid(img, 5)
-        gp = p.buildGaussianPyramid(img, 5)
+        gp = ctx.buildGaussianPyramid(img, 5)
     finally:
-        t.close()
-        p.close()
-    assert len(gt) == len(gp)
-    for i, (a, c) in enumerate(zip(gt, gp)):
-        assert a.tobytes() == c.tobytes(), f"plane {i} differs"
+        ctx.close()
+    ref = oracle.split_planes(oracle.fast_pyramid(img, 5), *shape, 5, 5)
+    assert len(gp) == len(ref)
+    for i, (a, c) in enumerate(zip(gp, ref)):
+        if a.tobytes() != c.tobytes():
+            bad = np.argwhere(a != c)
+            pytest.fail(f"plane {i} (octave {i // 5}, scale {i % 5}) {a.shape}: {len(bad)} values differ, "
+                        f"first at {bad[0].tolist()}: {a[tuple(bad[0])]!r} vs {c[tuple(bad[0])]!r}")
 
 
-@pytest.mark.parametrize("shape,b", [((1080, 1920), 0), ((203, 157), 2), ((33, 1200), 12),
-                                     ((300, 210), 3), ((130, 90), 6)])
-def test_fast_pyramid_close_to_exact(fctx_both, oracle, shape, b):
+@pytest.mark.parametrize("shape,b", SHAPES)
+def test_fast_pyramid_close_to_exact(fctx, siftgpu, oracle, shape, b):
     img = oracle.synth_image(b, *shape)
-    gp = fctx_both.buildGaussianPyramid(img, 5)
+    if shape[0] <= 1080 and shape[1] <= 1920:
+        gp = fctx.buildGaussianPyramid(img, 5)
+    else:
+        ctx = siftgpu.Context(*shape, 1, device=0, flags=FAST)
+        try:
+            gp = ctx.buildGaussianPyramid(img, 5)
+        finally:
+            ctx.close()
     ref = oracle.split_planes(oracle.build_gaussian_pyramid(img), *shape, 5, 5)
     errs = [float(np.abs(p.astype(np.float64) - q).max()) for p, q in zip(gp, ref)]
     assert max(errs) < PLANE_ATOL, errs
@@ -90,14 +76,34 @@ def test_fast_pyramid_close_to_exact(fctx_both, oracle, shape, b):
     assert errs[0] < 5e-4, errs[0]
 
 
-def test_fast_pyramid_border_rule(fctx_both):
+def test_fast_pyramid_border_rule(fctx):
     """The last source row and column never contribute (getSubMatrix, src/sift.cpp:116)."""
     img = np.zeros((64, 80), np.float32)
     img[-1, :] = 255
     img[:, -1] = 255
-    gp = fctx_both.buildGaussianPyramid(img, 3)
+    gp = fctx.buildGaussianPyramid(img, 3)
     for i, p in enumerate(gp):
         assert not p.any(), f"plane {i}"
+
+
+def test_fast_rejects_planes_past_the_offset_range(siftgpu):
+    """the separable kernel drops out-of-range loads and stores by
+    a 0x7f000000-byte offset, so an input whose rows span that range must be
+    refused (SIFT_E_SIZE) before any kernel runs, never silently mis-padded."""
+    import torch
+    ctx = siftgpu.Context(1080, 1920, 2, device=0, flags=FAST)
+    try:
+        imgs = torch.zeros((16,), dtype=torch.float32, device="cuda")
+        kp = torch.empty((16, 7), dtype=torch.int32, device="cuda")
+        de = torch.empty((16, 128), dtype=torch.float32, device="cuda")
+        offs = torch.empty((3,), dtype=torch.int32, device="cuda")
+        stride = (0x7f000000 // 4) // 1080 + 64  # 1080 rows of this stride pass the range
+        with pytest.raises(siftgpu.SiftError) as e:
+            ctx.detect_compute_batch(imgs.data_ptr(), 2, 1080, 1920, stride, 1080 * stride, kp.data_ptr(),
+                                     de.data_ptr(), 16, offs.data_ptr())
+        assert e.value.code == siftgpu.SIFT_E_SIZE, e.value
+    finally:
+        ctx.close()
 
 
 def _match(ka, da, kb, db):
@@ -156,10 +162,10 @@ def test_fast_1080p_match_rate(fctx, oracle):
     assert rate >= 0.95 and drate >= 0.9
 
 
-def test_fast_batch_equals_single(fctx, oracle):
+@pytest.mark.parametrize("B,R,C", [(3, 240, 320)])
+def test_fast_batch_equals_single(fctx, oracle, B, R, C):
     """Batch mode and the single-image path run the same kernels: bit-identical."""
     import torch
-    B, R, C = 3, 240, 320
     imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
     fctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=30)
     fctx.sync()
@@ -179,3 +185,33 @@ def test_fast_batch_equals_single(fctx, oracle):
         assert o[b + 1] - o[b] == len(ks)
         assert k[o[b]:o[b + 1]].tobytes() == np.ascontiguousarray(ks).view(np.uint8).tobytes()
         assert dd[o[b]:o[b + 1]].tobytes() == ds.tobytes()
+
+
+def test_fast_headline_batch_equals_single(siftgpu):
+    """configs[2] in fast mode: one 64 x 1080p batch call (other chunk seams
+    than a single image's launch) gives images 0, 31 and 63 bit-identical to
+    the single-image fast path, which test_fast_pyramid_equals_its_oracle pins."""
+    import torch
+    B, R, C = 64, 1080, 1920
+    ctx = siftgpu.Context(R, C, B, device=0, flags=FAST)
+    one = siftgpu.Context(R, C, 1, device=0, flags=FAST)
+    try:
+        imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
+        ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, seed_base=0)
+        cap = B * 40000
+        kpts = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
+        desc = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
+        offs = torch.empty((B + 1,), dtype=torch.int32, device="cuda")
+        ctx.detect_compute_batch(imgs.data_ptr(), B, R, C, C, R * C, kpts.data_ptr(), desc.data_ptr(), cap,
+                                 offs.data_ptr())
+        ctx.sync()
+        o = offs.cpu().numpy()
+        for b in (0, 31, 63):
+            ks, ds = one.SIFT_NCL(imgs[b].cpu().numpy())
+            assert o[b + 1] - o[b] == len(ks) > 5000
+            kb = kpts[o[b]:o[b + 1]].cpu().numpy().view(np.uint8).reshape(-1, 28)
+            assert kb.tobytes() == np.ascontiguousarray(ks).view(np.uint8).tobytes(), b
+            assert desc[o[b]:o[b + 1]].cpu().numpy().tobytes() == ds.tobytes(), b
+    finally:
+        ctx.close()
+        one.close()

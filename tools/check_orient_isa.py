@@ -117,14 +117,14 @@ def main():
     asm = sys.argv[1] if len(sys.argv) > 1 else compile_asm()
     s = open(asm).read()
     bad, found = [], 0
-    for m in re.finditer(r'^(_ZN4sift\S*orient_slots_kernel\S*):', s, re.M):
+    for m in re.finditer(r'^(_ZN4sift\S*orient_(?:slots_)?kernel\S*):', s, re.M):
         body = s[m.end():s.index('.Lfunc_end', m.end())].split('\n')
         errs, runs = check_kernel(m.group(1), body)
         found += 1
         print(f'{m.group(1)}: {runs} run(s) of 8 ordered steps, {len(errs)} violations')
         bad += errs
     if not found:
-        bad.append('no orient_slots_kernel in the assembly')
+        bad.append('no orientation kernel in the assembly')
     for e in bad:
         print('  ' + e)
     sys.exit(1 if bad else 0)
