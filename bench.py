@@ -136,9 +136,10 @@ print(len(k), time.perf_counter() - t0)
 
 
 def cpu_baseline_parallel(rows, cols, workers):
-    """Image-parallel all-cores rate: `workers`
-    independent processes, one image each, one thread each; rate = images /
-    wall.  Child processes import only the oracle (no GPU)."""
+    """Image-parallel rate on the GPU's share of the host (SURVEY.md 8(d) d4
+    item 2): `workers` (16: an eighth of the GPU box's CPUs) independent
+    processes, one image each, one thread each; rate = images / wall.  Child
+    processes import only the oracle (no GPU)."""
     O = _oracle()
     del O
     t0 = time.perf_counter()
@@ -160,7 +161,9 @@ def cpu_baseline_parallel(rows, cols, workers):
     nkp = sum(int(o[0]) for o in outs)
     per_img = [float(o[1]) for o in outs]
     mpix = workers * rows * cols / 1e6
+    nproc = os.cpu_count() or workers
     return {"value": round(mpix / wall, 4), "unit": "Mpix/s", "cores": workers, "kind": "port",
+            "cores_note": f"{workers} of {nproc} host CPUs: the per-GPU share of an 8-GPU node, not all cores",
             "keypoints_per_s": round(nkp / wall, 1), "seconds_wall": round(wall, 3),
             "seconds_per_image_median": round(float(np.median(per_img)), 3),
             "sample": f"{workers} synthetic {cols}x{rows} images (seeds 100..{99 + workers}), one process and "
@@ -459,9 +462,9 @@ def cpu_legs(a, errors):
     omp = guarded(errors, "cpu_baseline_omp", cpu_baseline, a.rows, a.cols, nthr)
     if omp is not None:
         cpu["cpu_baseline_omp"] = omp
-    par = guarded(errors, "cpu_baseline_all_cores", cpu_baseline_parallel, a.rows, a.cols, nthr)
+    par = guarded(errors, "cpu_baseline_gpu_share", cpu_baseline_parallel, a.rows, a.cols, nthr)
     if par:
-        cpu["cpu_baseline_all_cores"] = par
+        cpu["cpu_baseline_gpu_share"] = par
     cpu["cpu_host"] = {"nproc": os.cpu_count(), "model": _cpu_model(), "share_used": nthr,
                        "compiler_flags": "gcc -O3 -ffp-contract=off -fno-fast-math"}
     return cpu
@@ -487,7 +490,7 @@ class Part:
             def on_result(step, out, first=(b0 == 0)):
                 env.gathered["steps"] += 1 if first else 0
                 env.gathered["keypoints"] += sum(int(o[-1]) for o in out[1])
-            self.pipe = sift_dist.GatherPipeline(env.shard_batches(nb), self.cap, dst=0)
+            self.pipe = sift_dist.GatherPipeline(env.shard_batches(nb), self.cap, dst=0, timing=True)
             self.runner = sift_dist.PipelinedSteps(self.pipe, self.bufs, with_desc=False, on_result=on_result)
 
     def compute(self, k, d, o):
@@ -851,7 +854,10 @@ def main():
     res = {}
     if want("exact"):
         res["exact"] = run_exact(env)   # the headline: not guarded
-    if not a.no_fast and want("fast"):
+    # the fast leg only at N = 1: with collectives inside, a failure caught on
+    # one rank would leave the others waiting in that collective;
+    # the multi-GPU line is the exact path's
+    if not a.no_fast and want("fast") and world == 1:
         res["fast"] = guarded(errors, "fast", run_fast, env)
     if not (a.no_match or rank != 0 or env.B < 2 or res.get("exact") is None):
         res["match"] = guarded(errors, "match", run_match, env)
@@ -868,6 +874,10 @@ def main():
     env.close()
     if world > 1:
         dist.destroy_process_group()
+    # a GPU error caught in an optional leg leaves the line printed but the
+    # run marked failed: the context that raised it is not trusted further
+    if any(("hip" in v.lower() or "HIP" in v) for v in errors.values()):
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -531,8 +531,14 @@ int run_graphed(sift_ctx* c, const std::vector<char>& key, const std::vector<cha
       HIP_TRY(c, hipGraphLaunch(e.exec, c->stream));
       return SIFT_OK;
     }
+    // not updatable: the update may have patched some nodes before it
+    // failed, so this executable no longer matches its recorded buffers --
+    // drop the entry and instantiate a new executable below
     (void)hipGetLastError();
-    break;  // not updatable: instantiate a new executable below
+    (void)hipGraphExecDestroy(e.exec);
+    (void)hipGraphDestroy(e.graph);
+    c->graphs.erase(c->graphs.begin() + (long)i);
+    break;
   }
   sift_ctx::GraphEntry e;
   e.key = key;

@@ -1212,6 +1212,164 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
   }
 }
 
+// Orientation histograms, one wave per candidate, bins bucketed (round 4;
+// the one-image path).
+//
+// The reference's only ordering constraint (src/sift.cpp:429-437) is that each
+// bin receives its terms in window raster order; different bins are
+// independent chains.  orient_kernel walks a window one sample per step
+// (8 samples per batch, each added after the previous one's LDS round trip),
+// so a radius-17 window is a 1,225-step chain and one image's launch is as
+// long as its longest such walk.  Here a wave takes a candidate and 64
+// consecutive raster samples per batch: every lane forms its sample's bin and
+// value, the wave ranks each sample among the earlier samples of the same bin
+// (a 6-bit match over ballots), scatters the value to [rank][bin] in LDS, and
+// lane b (b < 36) then adds its bin's values in rank order into a register
+// accumulator that runs across the batches.  The chain is now the largest
+// per-batch bin count, summed over the batches, and every bin still gets
+// exactly the reference's adds in the reference's order.  Invalid samples
+// (outside the image interior, src/sift.cpp:405,410) join no bin; the masked
+// reads past a bin's count add +0.0 to a sum that is >= +0 (exact no-op).
+constexpr int kOBW = 4;  // waves per workgroup
+
+__global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
+  __shared__ float vals[kOBW][64][kOriBins];  // [wave][rank][bin]: owner reads are conflict free
+  __shared__ int cnt[kOBW][64];
+  __shared__ float hist[kOBW][kOriBins + 4], sm[kOBW][kOriBins + 4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int n = *A.cand_total;
+  if (n > A.cand_cap) n = A.cand_cap;
+  const ExpConsts ek = A.mc->e;
+  const float etab_lane = A.mc->exptab[lane];
+  const unsigned long long below = (1ull << lane) - 1ull;
+  cnt[w][lane] = 0;
+  // XCD-aware contiguous split of the raster-ordered candidates (speed only):
+  // XCD x takes [x per, (x + 1) per), its waves interleaved over them
+  const int nw = (int)(gridDim.x >> 3) * kOBW;
+  const int per = (n + 7) / 8;
+  const int xcd = blockIdx.x & 7, wid = (int)(blockIdx.x >> 3) * kOBW + w;
+  const int cend = min(n, (xcd + 1) * per);
+  for (int ci = xcd * per + wid; ci < cend; ci += nw) {
+    const CandOut& co = A.couts[ci];
+    if (co.npeaks == 0) {  // refinement rejected it
+      if (lane == 0) A.npeaks[ci] = 0;
+      continue;
+    }
+    const int o = A.cands[ci].ol & 255;
+    const Octave& O = A.L.oct[o];
+    const int pitch = O.pitch, rr = co.ref_r, rc = co.ref_c;
+    // ---- calcOrientationHist, src/sift.cpp:389-437 ----
+    const float scl = co.size * 0.5f / (1 << o);
+    const int radius = cv_round(3 * 1.5f * scl);
+    const float sigma = 1.5f * scl;
+    const float escale = -1.f / (2.f * sigma * sigma);
+    const float2* gwin = A.grad + co.img * A.L.g_img + O.g_off[co.ref_layer];
+    const int D = 2 * radius + 1, ns = D * D;
+    // lane's sample index base + lane as (si, sj) of the D x D window, moved
+    // on by 64 = q D + rem per batch
+    int si = lane / D, sj = lane - (lane / D) * D;
+    const int q64 = 64 / D, r64 = 64 - q64 * D;
+    float acc = 0.f;  // lane b < 36: bin b's running sum
+    // the batch at (si, sj): validity and the gather (issued one batch ahead,
+    // so its latency runs under the previous batch's bucketing)
+    auto gather = [&](int base_, bool& ok_, float2& mo_) {
+      const int y = rr + si - radius, x = rc + sj - radius;
+      ok_ = base_ + lane < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
+      mo_ = gwin[ok_ ? (long long)y * pitch + x : (long long)rr * pitch + rc];  // (Mag, Ori)
+    };
+    auto step64 = [&]() {
+      si += q64;
+      sj += r64;
+      if (sj >= D) {
+        sj -= D;
+        ++si;
+      }
+    };
+    bool ok_n;
+    float2 mo_n;
+    gather(0, ok_n, mo_n);
+    for (int base = 0; base < ns; base += 64) {
+      const int i = si - radius, j = sj - radius;
+      const bool ok = ok_n;
+      const float2 mo = mo_n;
+      step64();
+      if (base + 64 < ns) gather(base + 64, ok_n, mo_n);
+      // |argument| <= 2 * 17^2 / (2 * 2.85^2) < 36: exp32f's input clamp never acts
+      const float wgt = exp32f_v<false>((i * i + j * j) * escale, etab_lane, ek);
+      int bin = cv_round((kOriBins / 360.f) * mo.y);
+      if (bin >= kOriBins) bin -= kOriBins;
+      if (bin < 0) bin += kOriBins;
+      const float val = wgt * mo.x;
+      const int key = ok ? bin : 63;
+      // lanes with the same key: match over the key's 6 bits
+      unsigned long long m = ~0ull;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const unsigned long long bk = __ballot((key >> k) & 1);
+        m &= ((key >> k) & 1) ? bk : ~bk;
+      }
+      const int rank = __popcll(m & below), total = __popcll(m);
+      if (ok) {
+        vals[w][rank][key] = val;
+        if (rank == total - 1) cnt[w][key] = total;
+      }
+      wave_sync();
+      int c = 0;
+      if (lane < kOriBins) {
+        c = cnt[w][lane];
+        cnt[w][lane] = 0;
+      }
+      // bin lane's values in rank (= raster) order, 4 reads in flight
+      for (int r = 0; __ballot(r < c); r += 4) {
+        float v4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v4[u] = (r + u < c) ? vals[w][r + u][lane] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = acc + v4[u];
+      }
+      wave_sync();
+    }
+    // ---- smoothing (src/sift.cpp:440-451), max, peaks (src/sift.cpp:524-541) ----
+    if (lane < kOriBins) hist[w][lane] = acc;
+    wave_sync();
+    float h = -1.f;
+    if (lane < kOriBins) {
+      const float* th = hist[w];
+      const int t = lane;
+      const int jm2 = (t + kOriBins - 2) % kOriBins, jp2 = (t + 2) % kOriBins;
+      const int jm1 = (t + kOriBins - 1) % kOriBins, jp1 = (t + 1) % kOriBins;
+      h = (th[jm2] + th[jp2]) * (1.f / 16.f) + (th[jm1] + th[jp1]) * (4.f / 16.f) + th[t] * (6.f / 16.f);
+      sm[w][t] = h;
+    }
+    float mx = h;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) mx = fmaxf(mx, __shfl_xor(mx, k));
+    wave_sync();
+    const float mag_thr = (float)(mx * 0.8f);
+    bool pk = false;
+    float ang = 0.f;
+    if (lane < kOriBins) {
+      const int t = lane;
+      const int l = t > 0 ? t - 1 : kOriBins - 1;
+      const int r2 = t < kOriBins - 1 ? t + 1 : 0;
+      const float hl = sm[w][l], hr = sm[w][r2];
+      if (h > hl && h > hr && h >= mag_thr) {
+        float bn = t + 0.5f * (hl - hr) / (hl - 2 * h + hr);
+        bn = bn < 0 ? kOriBins + bn : bn >= kOriBins ? bn - kOriBins : bn;
+        float a = 360.f - (float)((360.f / kOriBins) * bn);
+        if (fabsf(a - 360.f) < FLT_EPSILON) a = 0.f;
+        ang = a;
+        pk = true;
+      }
+    }
+    const unsigned long long pmask = __ballot(pk);
+    CandOut* cw = A.couts + ci;
+    if (pk) cw->angle[__popcll(pmask & below)] = ang;
+    if (lane == 0) A.npeaks[ci] = __popcll(pmask);
+    wave_sync();
+  }
+}
+
 // Orientation histograms, kOSlots candidates per lane group (default kernel).
 //
 // orient_kernel above is bound by its histogram chain: a group's 8 samples of a
@@ -1466,17 +1624,22 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.couts = D.couts;
   A.npeaks = D.npeaks;
   hipLaunchKernelGGL(refine_kernel, dim3(resident_grid((const void*)refine_kernel, 256, 0, 2048)), dim3(256), 0, st, A);
-  // slots per lane group: 2 for batches; 1 (the one-candidate-per-group
-  // orient_kernel: twice the waves) for one image, whose launch leaves most
-  // SIMDs with one wave (round 3: 0.93 vs 0.95 ms per 1080p image);
-  // SIFT_HIP_ORIENT_SLOTS=1..4 forces a variant (A/B runs)
+  // batches: two candidates per lane group (orient_slots_kernel<2>); one
+  // image: one wave per candidate with bucketed bins (orient_bin_kernel,
+  // round 4), whose chain is a window's largest per-batch bin counts instead
+  // of its whole sample walk.  SIFT_HIP_ORIENT_SLOTS=1 (orient_kernel),
+  // 2..4 (orient_slots_kernel<n>) or 5 (orient_bin_kernel) forces a variant
+  // (A/B runs; every variant is bit-identical, tests/test_gpu_parity.py)
   static const int slots_env = [] {
     const char* e = getenv("SIFT_HIP_ORIENT_SLOTS");
     const int v = e ? atoi(e) : 0;
-    return v >= 1 && v <= 4 ? v : 0;
+    return v >= 1 && v <= 5 ? v : 0;
   }();
-  const int slots = slots_env ? slots_env : batch == 1 ? 1 : 2;
-  if (slots == 1)
+  const int slots = slots_env ? slots_env : batch == 1 ? 5 : 2;
+  if (slots == 5)
+    hipLaunchKernelGGL(orient_bin_kernel, dim3(resident_grid((const void*)orient_bin_kernel, 64 * kOBW, 0, 2048)),
+                       dim3(64 * kOBW), 0, st, A);
+  else if (slots == 1)
     hipLaunchKernelGGL(orient_kernel, dim3(resident_grid((const void*)orient_kernel, 64, 0, 8192)), dim3(64), 0, st,
                        A);
   else if (slots == 3)

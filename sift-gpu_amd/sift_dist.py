@@ -62,7 +62,8 @@ class GatherPipeline:
     and once at the end pipe.gather(last slot, ...).
     """
 
-    def __init__(self, batches: list[int], cap: int, dst: int = 0, slots: int = 2, meta_group="auto"):
+    def __init__(self, batches: list[int], cap: int, dst: int = 0, slots: int = 2, meta_group="auto",
+                 timing: bool = False):
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
         assert len(batches) == self.world
         self.batches, self.cap, self.dst = list(batches), cap, dst
@@ -79,7 +80,12 @@ class GatherPipeline:
         self.gathers = 0
         self.recv_counts = [0] * self.world   # records received from each rank (dst only)
         self.sent_records = 0                 # records this rank sent (rank != dst)
-        self._spans = []                      # (start, end) device events of each transfer group
+        # (start, end) device events of each transfer group: only with
+        # timing=True (bench.py), folded into _span_ms once complete so a long
+        # run keeps a bounded list
+        self.timing = timing
+        self._spans = []
+        self._span_ms = 0.0
 
     # -- compute side ---------------------------------------------------------
     def wait_slot(self, s: int):
@@ -142,13 +148,17 @@ class GatherPipeline:
         if self.cuda:
             self.side.wait_event(self.ready[s])
             with torch.cuda.stream(self.side):
-                t0 = torch.cuda.Event(enable_timing=True)
-                t0.record(self.side)
+                t0 = None
+                if self.timing:
+                    t0 = torch.cuda.Event(enable_timing=True)
+                    t0.record(self.side)
                 post()
-                ev = torch.cuda.Event(enable_timing=True)
+                ev = torch.cuda.Event(enable_timing=self.timing)
                 ev.record(self.side)
                 self.done[s] = ev
-                self._spans.append((t0, ev))
+                if self.timing:
+                    self._spans.append((t0, ev))
+                    self._fold_spans()
         else:
             post()
         if self.rank != self.dst:
@@ -167,10 +177,18 @@ class GatherPipeline:
         if self.cuda:
             self.side.synchronize()
 
+    def _fold_spans(self, keep: int = 8):
+        """Adds the completed transfer spans (all but the newest `keep`) into
+        _span_ms and drops their events."""
+        while len(self._spans) > keep and self._spans[0][1].query():
+            a, b = self._spans.pop(0)
+            self._span_ms += a.elapsed_time(b)
+
     def reset_stats(self):
         self.gathers, self.sent_records = 0, 0
         self.recv_counts = [0] * self.world
         self._spans = []
+        self._span_ms = 0.0
 
     def stats(self) -> dict:
         """Per-rank gather evidence since the last reset_stats(); call after
@@ -178,8 +196,8 @@ class GatherPipeline:
         transfer groups (each from its start, i.e. after the step's compute,
         to the last receive/send completing)."""
         ms = None
-        if self.cuda and self._spans:
-            ms = sum(a.elapsed_time(b) for a, b in self._spans)
+        if self.cuda and self.timing:
+            ms = self._span_ms + sum(a.elapsed_time(b) for a, b in self._spans)
         return {"backend": dist.get_backend(), "world_size": self.world, "rank": self.rank,
                 "gathers": self.gathers, "received_records_per_rank": list(self.recv_counts),
                 "sent_records": self.sent_records, "transfer_ms": ms}

@@ -74,7 +74,7 @@ def test_line_survives_failing_cpu_leg(bench, monkeypatch, capsys):
         monkeypatch.setattr(bench, leg, lambda *a, **k: None)
     out = _run(bench, monkeypatch, capsys, [])
     assert out["value"] > 0 and out["cpu_baseline"]["value"] == 0.6
-    assert "cpu_baseline_all_cores" not in out and "cpu leg hung" in out["leg_errors"]["cpu_baseline_all_cores"]
+    assert "cpu_baseline_gpu_share" not in out and "cpu leg hung" in out["leg_errors"]["cpu_baseline_gpu_share"]
 
 
 def test_line_survives_failing_block(bench, monkeypatch, capsys):

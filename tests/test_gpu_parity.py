@@ -403,7 +403,8 @@ print(len(kps), sha(kps), sha(desc))
 
 @pytest.mark.parametrize("env", [{"SIFT_HIP_EXTREMA_TILES": "1"}, {"SIFT_HIP_ORIENT_SLOTS": "1"},
                                  {"SIFT_HIP_ORIENT_SLOTS": "2"}, {"SIFT_HIP_ORIENT_SLOTS": "3"},
-                                 {"SIFT_HIP_ORIENT_SLOTS": "4"}, {"SIFT_HIP_DESC_PACKED": "0"},
+                                 {"SIFT_HIP_ORIENT_SLOTS": "4"}, {"SIFT_HIP_ORIENT_SLOTS": "5"},
+                                 {"SIFT_HIP_DESC_PACKED": "0"},
                                  {"SIFT_HIP_FUSE_DEC": "0"}, {"SIFT_HIP_DESC_DEEP": "0"}])
 def test_kernel_variants_match_golden(env):
     """The A/B kernel variants the library keeps behind environment switches
