@@ -47,11 +47,6 @@ Layout make_layout(int rows, int cols, int n_oct) {
 int resident_grid(const void* kernel, int block, size_t lds, int fixed_grid) {
   static std::mutex mu;
   static std::map<std::pair<const void*, int>, int> cache;
-  static const bool fixed = [] {
-    const char* e = getenv("SIFT_HIP_FIXED_GRID");
-    return e && atoi(e) != 0;
-  }();
-  if (fixed) return fixed_grid;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return fixed_grid;
   std::lock_guard<std::mutex> lk(mu);

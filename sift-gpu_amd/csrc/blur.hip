@@ -598,14 +598,14 @@ __device__ __forceinline__ void sym_walk(const SymArgs& A, int slot, int local, 
 
 // Waves are independent (one 64-lane workgroup each).  The octave kernel's
 // slots run in launch order, widest kernel first: slot s blurs scale 4 - s.
-// OCC = 3 (default): the kernel holds 168 VGPRs, 3 waves per SIMD instead of
-// the 4 its 101 allow.  Alone it runs as fast (3 waves keep the 2-cycle VALU
-// issue full); beside another stream's latency-bound kernels (bench.py's 2
-// streams) the step is 3-4 % shorter, measured (SIFT_HIP_SYM_OCC=4 restores 4).
-template <int OCC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void blur_sym_kernel(SymArgs A) {
+// The kernel holds 168 VGPRs, 3 waves per SIMD instead of the 4 its 101
+// allow.  Alone it runs as fast (3 waves keep the 2-cycle VALU issue full);
+// beside another stream's latency-bound kernels (bench.py's 2 streams) the
+// step is 3-4 % shorter, measured in rounds 2-3 (4 waves per SIMD: 6,448-6,499
+// vs 6,513-6,552 Mpix/s).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void blur_sym_kernel(SymArgs A) {
   __shared__ float ring[kSymRing];
-  if constexpr (OCC == 3) asm volatile("; hold v160-v167" ::: "v160", "v167");
+  asm volatile("; hold v160-v167" ::: "v160", "v167");
   const int wid = blockIdx.x;
   const int slot = wid >= A.start[3] ? 3 : wid >= A.start[2] ? 2 : wid >= A.start[1] ? 1 : 0;
   const int local = wid - A.start[slot];
@@ -659,11 +659,6 @@ static double sym_row_cost(int w) { return (2. * w + 1) * (w + 1) + (2. * w + 1)
 // images per launch, as on one of bench.py's 4 streams: 270-row chunks).
 // Taller chunks recompute less halo (w rows above and below a chunk); the
 // other slots get chunks of about the same work (rows x row cost).
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 static int sym_simds() {
   static const int n = [] {
     int dev = 0, cus = 0;
@@ -676,12 +671,11 @@ static int sym_simds() {
 }
 
 static void sym_plan(SymArgs& A, const int* w, int nslot, double cp) {
-  static const int force = env_int("SIFT_HIP_SYM_ROWS", 0);
   double total = 0;
   for (int s = 0; s < nslot; ++s) total += (double)A.strips * A.batch * A.rows * sym_row_cost(w[s]);
   // longest wave (rows_w0 x cost x 4 cycles) <= cp x whole-chip time (total x 2 cycles / SIMDs)
   int rows_w0 = (int)(cp * total / (2.0 * sym_simds() * sym_row_cost(w[0])));
-  rows_w0 = force > 0 ? force : std::max(64, rows_w0);
+  rows_w0 = std::max(64, rows_w0);
   const double per = sym_row_cost(w[0]) * rows_w0;
   int start = 0;
   for (int s = 0; s < nslot; ++s) {
@@ -727,16 +721,8 @@ void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr,
   A.strips = (O.cols + 63) / 64;
   A.batch = batch;
   const int w[4] = {kSymW4, kSymW3, kSymW2, kSymW1};
-  static const double cp = [] {
-    const char* e = getenv("SIFT_HIP_SYM_CP");
-    return e ? atof(e) : 0.7;
-  }();
-  sym_plan(A, w, 4, cp);
-  static const int occ = env_int("SIFT_HIP_SYM_OCC", 3);
-  if (occ == 4)
-    hipLaunchKernelGGL(blur_sym_kernel<4>, dim3(A.start[4]), dim3(64), 0, st, A);
-  else
-    hipLaunchKernelGGL(blur_sym_kernel<3>, dim3(A.start[4]), dim3(64), 0, st, A);
+  sym_plan(A, w, 4, 0.7);
+  hipLaunchKernelGGL(blur_sym_kernel, dim3(A.start[4]), dim3(64), 0, st, A);
 }
 
 // ---- resize INTER_NEAREST to the next octave (src/sift.cpp:252-254) -------

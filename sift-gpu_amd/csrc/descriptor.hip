@@ -30,10 +30,9 @@
 
 #include <type_traits>
 
-// waves per SIMD the batch descriptor kernel is compiled for (register budget)
-#ifndef DESC_WPE
-#define DESC_WPE 4
-#endif
+// waves per SIMD the batch descriptor kernel is compiled for (register budget;
+// 3 with no spills measured 8.4-8.5 vs 7.6 ms, round 3)
+constexpr int kDescWpe = 4;
 
 namespace sift {
 
@@ -113,12 +112,11 @@ struct RecT<true> {
 // image, round 3): its gather is issued a step earlier, so a wave that is
 // alone on its SIMD does not wait a full memory latency per batch.
 template <bool PACKED, bool DET, int PF = 1>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF == 2 ? 2 : PACKED ? DESC_WPE : 1))) void
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF == 2 ? 2 : PACKED ? kDescWpe : 1))) void
 descriptor_kernel(DescArgs A) {
   __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
   // per-sample hand-off records (see RecT)
   __shared__ __attribute__((aligned(16))) float rec[PACKED ? kGrp * kRecG : 8 * kRecStride2];
-  __shared__ __attribute__((aligned(16))) unsigned char recq[PACKED ? 64 * 8 : 16];
   // per row: (jlo + 64) | len << 16 (PACKED: << 8, 16 bits)
   __shared__ typename std::conditional<PACKED, unsigned short, int>::type rows_tab[kGrp][kMaxWinRows];
   constexpr int kLenSh = PACKED ? 8 : 16, kLoMask = PACKED ? 0xff : 0xffff;
@@ -383,6 +381,7 @@ descriptor_kernel(DescArgs A) {
       enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
     };
     int odd_cur = 0;
+    uint2 qq_cur = make_uint2(0u, 0u);  // PACKED: this owner's 8 bin bytes of the batch
     Loc loc_nxt;  // PF = 2: batch k + 1, located and gathering
     if (nmax > 0) {
       if constexpr (PF == 2) {
@@ -411,11 +410,34 @@ descriptor_kernel(DescArgs A) {
         // 7.45-7.47 ms: it is bound by VALU issue, not by the conflicts.)
         char* rb = reinterpret_cast<char*>(rec);
         const int wv = ((g << 8) | ((q << 2) ^ ((g & 1) << 4))) | (odd_cur << 5);
-        const int wq = ((g << 6) | q) | (odd_cur << 3);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          *reinterpret_cast<float*>(rb + (wv ^ (k << 5))) = rc_cur.v[k];
-          recq[wq ^ (k << 3)] = (unsigned char)(rc_cur.qb[k >> 2] >> (8 * (k & 3)));
+        for (int k = 0; k < 8; ++k) *reinterpret_cast<float*>(rb + (wv ^ (k << 5))) = rc_cur.v[k];
+        // bin bytes to their owners in registers (round 4; were eight
+        // ds_write_b8 per lane and one ds_read_b64): byte s of this lane's
+        // pair <- corner s ^ odd, then an 8 x 8 byte transpose over the group's
+        // lanes (lane bit b <-> byte bit b: DPP row shifts by 4, quad perms,
+        // v_perm_b32), so owner s holds sample q's bin byte at byte q
+        {
+          unsigned w0 = (odd_cur & 4) ? rc_cur.qb[1] : rc_cur.qb[0];
+          unsigned w1 = (odd_cur & 4) ? rc_cur.qb[0] : rc_cur.qb[1];
+          const unsigned sx = 0x03020100u ^ ((unsigned)(odd_cur & 3) * 0x01010101u);
+          w0 = __builtin_amdgcn_perm(w0, w0, sx);
+          w1 = __builtin_amdgcn_perm(w1, w1, sx);
+          const unsigned a = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w0, 0x104, 0xf, 0xf, false);  // lane + 4
+          const unsigned c = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0x114, 0xf, 0xf, false);  // lane - 4
+          if (q & 4)
+            w0 = c;
+          else
+            w1 = a;
+          const unsigned s2 = (q & 2) ? 0x03020706u : 0x05040100u;
+          unsigned p0 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w0, 0x4E, 0xf, 0xf, false);  // lane ^ 2
+          unsigned p1 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0x4E, 0xf, 0xf, false);
+          w0 = __builtin_amdgcn_perm(p0, w0, s2);
+          w1 = __builtin_amdgcn_perm(p1, w1, s2);
+          const unsigned s1 = (q & 1) ? 0x03070105u : 0x06020400u;
+          p0 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w0, 0xB1, 0xf, 0xf, false);  // lane ^ 1
+          p1 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0xB1, 0xf, 0xf, false);
+          qq_cur = make_uint2(__builtin_amdgcn_perm(p0, w0, s1), __builtin_amdgcn_perm(p1, w1, s1));
         }
       } else {
         float2* dst2 = reinterpret_cast<float2*>(rec + q * kRecStride2 + g * 16);
@@ -442,7 +464,7 @@ descriptor_kernel(DescArgs A) {
         const int rv = (g << 8) | (q << 5);  // samples 0-3 at bit 4 = g & 1, samples 4-7 at the other half
         const float4 va = *reinterpret_cast<const float4*>(rb + (rv | ((g & 1) << 4)));
         const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | (((g & 1) ^ 1) << 4)));
-        const uint2 qq = *reinterpret_cast<const uint2*>(recq + lane * 8);
+        const uint2 qq = qq_cur;
         const float vals[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {

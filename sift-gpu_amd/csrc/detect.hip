@@ -798,11 +798,7 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
     // (a chunk re-reads 2 rows)
     long long strip_rows = 0;
     for (int o = 0; o < L.n_oct; ++o) strip_rows += (long long)((L.oct[o].cols + 63) / 64) * L.oct[o].rows;
-    static const long long target = [] {
-      const char* e = getenv("SIFT_HIP_EXTREMA_WAVES");  // tuning knob (A/B runs)
-      const long long v = e ? atoll(e) : 65536;
-      return v > 0 ? v : 65536;
-    }();
+    constexpr long long target = 65536;  // waves per launch (16 K / 32 K / 64 K measured in round 2)
     W.chunk = (int)std::min<long long>(512, std::max<long long>(8, strip_rows * batch / target));
     int w = 0;
     for (int o = 0; o < L.n_oct; ++o) {
