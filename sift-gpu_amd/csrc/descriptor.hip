@@ -270,50 +270,70 @@ descriptor_kernel(DescArgs A) {
     // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
     // the owner adds its lane to form the [qidx][lane] address.
     RecT<PACKED> rc_cur;  // (qidx, val) x 8 corners of this lane's sample
-    // locate: the sample at the walk position, its bins and its gather (in
-    // flight until finish uses it); finish: the weights and corner records.
+    // locate: the sample at the walk position, its gather (in flight until
+    // finish uses it) and the parts of its record that do not need the pixel
+    // (weight, spatial bins); finish: the rest.
     struct Loc {
-      float c_rot, r_rot, rbin, cbin;
+      float w, rbin, cbin;  // Gaussian weight; fractional spatial bin parts
+      int Rm, Cm;           // interior base corner (0 for an invalid sample)
       float2 mo_raw;
       bool ok;
     };
     auto locate = [&](bool in_range, Loc& L) {
       const int i = ri - radius, j = rlo + u;
-      L.c_rot = j * cos_t - i * sin_t;
-      L.r_rot = j * sin_t + i * cos_t;
-      L.rbin = L.r_rot + d / 2 - 0.5f;
-      L.cbin = L.c_rot + d / 2 - 0.5f;
+      const float c_rot = j * cos_t - i * sin_t;
+      const float r_rot = j * sin_t + i * cos_t;
+      float rbin = r_rot + d / 2 - 0.5f;
+      float cbin = c_rot + d / 2 - 0.5f;
       const int r = py + i, c = px + j;
       // the row table enumerates interior pixels only (src/sift.cpp:620-621's
       // 0 < r < rows-1, 0 < c < cols-1), so only the whole-window walk tests them
-      L.ok = in_range && L.rbin > -1 && L.rbin < d && L.cbin > -1 && L.cbin < d &&
+      L.ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d &&
              (table || (r > 0 && r < rows - 1 && c > 0 && c < cols - 1));
       // an invalid sample gathers from the clamped keypoint centre (any valid
       // address: its value is replaced below); plane offsets fit 32 bits
-      L.mo_raw = gimg[(unsigned)(L.ok ? r * pitch32 + c : ctr_off)];  // (Mag, Ori) of the pixel
+      L.mo_raw = gimg[(unsigned)(L.ok ? __mul24(r, pitch32) + c : ctr_off)];  // (Mag, Ori) of the pixel
+      L.w = exp32f_v<false>((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
+      // cvFloor: |rbin|, |cbin| < 10, so floorf is exact and (int)floorf ==
+      // cvFloor; rbin - floorf(rbin) == rbin - (float)r0
+      const float fr = floorf(rbin), fc = floorf(cbin);
+      L.rbin = rbin - fr;
+      L.cbin = cbin - fc;
+      // interior coordinates of the base corner: Rm = R0 - 1 = r0 in [-1, 3]
+      L.Rm = L.ok ? (int)fr : 0;
+      L.Cm = L.ok ? (int)fc : 0;
     };
     auto finish = [&](const Loc& L, RecT<PACKED>& out, int& odd_out) {
-      const float c_rot = L.c_rot, r_rot = L.r_rot;
-      float rbin = L.rbin, cbin = L.cbin;
+      const float rbin = L.rbin, cbin = L.cbin;
       const bool ok = L.ok;
       // invalid: (0, 0) -- border gradients are never written and may hold NaN
       const float2 mo = ok ? L.mo_raw : make_float2(0.f, 0.f);
-      const float w = exp32f_v<false>((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
       float obin = (mo.y - ori) * bins_per_rad;
-      const float mag = mo.x * w;
-      // cvFloor: |rbin|, |cbin|, |obin| < 10, so floorf is exact and
-      // (int)floorf == cvFloor; rbin - floorf(rbin) == rbin - (float)r0
-      const float fr = floorf(rbin), fc = floorf(cbin), fo = floorf(obin);
-      int r0 = (int)fr, c0 = (int)fc;
+      const float mag = mo.x * L.w;
+      const float fo = floorf(obin);  // |obin| < 10: exact, as above
       int o0 = (int)fo;
-      rbin -= fr;
-      cbin -= fc;
       obin -= fo;
       if (o0 < 0) o0 += nb;
       if (o0 >= nb) o0 -= nb;
-      const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-      const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-      const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+      const int Rm = L.Rm, Cm = L.Cm, O0 = ok ? o0 : 0;
+      const int odd = ((Rm & 1) << 2) | ((Cm & 1) << 1) | (O0 & 1);
+      float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+      if constexpr (PACKED) {
+        // corners outside the interior rows carry +0.0 (added to some interior
+        // bin: an exact no-op, every bin is >= +0) instead of going to a
+        // trash bin; each weight is masked after every product that uses its
+        // unmasked value, so the interior corners' values are unchanged
+        v_r0 = Rm >= 0 ? v_r0 : 0.f;
+        v_r1 = Rm <= 2 ? v_r1 : 0.f;
+      }
+      float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+      float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+      if constexpr (PACKED) {  // and outside the interior columns
+        v_rc00 = Cm >= 0 ? v_rc00 : 0.f;
+        v_rc10 = Cm >= 0 ? v_rc10 : 0.f;
+        v_rc01 = Cm <= 2 ? v_rc01 : 0.f;
+        v_rc11 = Cm <= 2 ? v_rc11 : 0.f;
+      }
       float v[8];
       v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
       v[6] = v_rc11 - v[7];
@@ -323,25 +343,39 @@ descriptor_kernel(DescArgs A) {
       v[2] = v_rc01 - v[3];
       v[1] = v_rc00 * obin;
       v[0] = v_rc00 - v[1];
-      // interior coordinates of the base corner: Rm = R0 - 1 = r0 in [-1, 3]
-      const int Rm = ok ? r0 : 0, Cm = ok ? c0 : 0, O0 = ok ? o0 : 0;
-      const int odd = ((Rm & 1) << 2) | ((Cm & 1) << 1) | (O0 & 1);
-      // corner k's bin index qidx_k (independent of the owner); the store
-      // places it in owner slot k ^ odd, so no value permutation here
-      const int qi0 = (Rm >> 1) * 10 + (Cm >> 1) * 5 + (O0 >> 1);
-      const int a10 = (Rm & 1) ? 10 : 0, a5 = (Cm & 1) ? 5 : 0, a1 = O0 & 1;
-      const bool r0v = Rm >= 0, r1v = Rm <= 2, c0v = Cm >= 0, c1v = Cm <= 2;
-      const int q1 = qi0 + a1, q2 = qi0 + a5, q4 = qi0 + a10;
-      const int qk[8] = {r0v && c0v ? qi0 : kTrash,      r0v && c0v ? q1 : kTrash,
-                         r0v && c1v ? q2 : kTrash,       r0v && c1v ? q2 + a1 : kTrash,
-                         r1v && c0v ? q4 : kTrash,       r1v && c0v ? q4 + a1 : kTrash,
-                         r1v && c1v ? q4 + a5 : kTrash,  r1v && c1v ? q4 + a5 + a1 : kTrash};
       if constexpr (PACKED) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) out.v[k] = v[k];
-        out.qb[0] = qk[0] | (qk[1] << 8) | (qk[2] << 16) | (qk[3] << 24);
-        out.qb[1] = qk[4] | (qk[5] << 8) | (qk[6] << 16) | (qk[7] << 24);
+        // bin bytes in owner-slot order: byte s (word s >> 2) is the qidx of
+        // corner k = s ^ odd, whose R = Rm + (s2 ^ (Rm & 1)) is even for s2 = 0
+        // and odd for s2 = 1 (likewise C with s1, O with s0), so
+        //   qidx = Rpart[s2] + Cpart[s1] + Opart[s0]
+        // with (x = Rm + 1, y = Cm + 1 in [0, 4]) Rpart[0] = T_R[x + 1],
+        // Rpart[1] = T_R[x], T_R = {0, 0, 0, 10, 10, 10}; Cpart likewise from
+        // T_C = {0, 0, 0, 5, 5, 5}; Opart[0] = (O0 + 1) >> 1, Opart[1] = O0 >> 1.
+        // The tables are byte lookups (v_perm_b32 over the 8-byte table);
+        // their entries for a row / column outside the interior are arbitrary
+        // interior bins (those corners carry +0.0, above).
+        // (byte replication by v_perm_b32 with selector 0)
+        const unsigned x = (unsigned)(Rm + 1), y = (unsigned)(Cm + 1);
+        const unsigned selR1 = __builtin_amdgcn_perm(0u, x, 0u), selR0 = selR1 + 0x01010101u;
+        const unsigned selC = __builtin_amdgcn_perm(0u, y, 0u) + 0x00000101u;
+        const unsigned po = (unsigned)(O0 & 1);
+        const unsigned o4 = __builtin_amdgcn_perm(0u, (unsigned)(O0 >> 1), 0u) + (po | (po << 16));
+        const unsigned c4 = __builtin_amdgcn_perm(0x00000505u, 0x05000000u, selC) + o4;
+        out.qb[0] = __builtin_amdgcn_perm(0x00000a0au, 0x0a000000u, selR0) + c4;
+        out.qb[1] = __builtin_amdgcn_perm(0x00000a0au, 0x0a000000u, selR1) + c4;
       } else {
+        // corner k's bin index qidx_k (independent of the owner); the store
+        // places it in owner slot k ^ odd, so no value permutation here
+        const int qi0 = __mul24(Rm >> 1, 10) + (Cm >> 1) * 5 + (O0 >> 1);
+        const int a10 = (Rm & 1) ? 10 : 0, a5 = (Cm & 1) ? 5 : 0, a1 = O0 & 1;
+        const bool r0v = Rm >= 0, r1v = Rm <= 2, c0v = Cm >= 0, c1v = Cm <= 2;
+        const int q1 = qi0 + a1, q2 = qi0 + a5, q4 = qi0 + a10;
+        const int qk[8] = {r0v && c0v ? qi0 : kTrash,      r0v && c0v ? q1 : kTrash,
+                           r0v && c1v ? q2 : kTrash,       r0v && c1v ? q2 + a1 : kTrash,
+                           r1v && c0v ? q4 : kTrash,       r1v && c0v ? q4 + a1 : kTrash,
+                           r1v && c1v ? q4 + a5 : kTrash,  r1v && c1v ? q4 + a5 + a1 : kTrash};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           out.r[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
@@ -414,29 +448,25 @@ descriptor_kernel(DescArgs A) {
         for (int k = 0; k < 8; ++k) *reinterpret_cast<float*>(rb + (wv ^ (k << 5))) = rc_cur.v[k];
         // bin bytes to their owners in registers (round 4; were eight
         // ds_write_b8 per lane and one ds_read_b64): byte s of this lane's
-        // pair <- corner s ^ odd, then an 8 x 8 byte transpose over the group's
+        // pair is corner s ^ odd's (finish), then an 8 x 8 byte transpose over the group's
         // lanes (lane bit b <-> byte bit b: DPP row shifts by 4, quad perms,
         // v_perm_b32), so owner s holds sample q's bin byte at byte q
         {
-          unsigned w0 = (odd_cur & 4) ? rc_cur.qb[1] : rc_cur.qb[0];
-          unsigned w1 = (odd_cur & 4) ? rc_cur.qb[0] : rc_cur.qb[1];
-          const unsigned sx = 0x03020100u ^ ((unsigned)(odd_cur & 3) * 0x01010101u);
-          w0 = __builtin_amdgcn_perm(w0, w0, sx);
-          w1 = __builtin_amdgcn_perm(w1, w1, sx);
-          const unsigned a = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w0, 0x104, 0xf, 0xf, false);  // lane + 4
-          const unsigned c = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0x114, 0xf, 0xf, false);  // lane - 4
+          unsigned w0 = rc_cur.qb[0], w1 = rc_cur.qb[1];
+          const unsigned a = (unsigned)__builtin_amdgcn_mov_dpp((int)w0, 0x104, 0xf, 0xf, true);  // lane + 4
+          const unsigned c = (unsigned)__builtin_amdgcn_mov_dpp((int)w1, 0x114, 0xf, 0xf, true);  // lane - 4
           if (q & 4)
             w0 = c;
           else
             w1 = a;
           const unsigned s2 = (q & 2) ? 0x03020706u : 0x05040100u;
-          unsigned p0 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w0, 0x4E, 0xf, 0xf, false);  // lane ^ 2
-          unsigned p1 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0x4E, 0xf, 0xf, false);
+          unsigned p0 = (unsigned)__builtin_amdgcn_mov_dpp((int)w0, 0x4E, 0xf, 0xf, true);  // lane ^ 2
+          unsigned p1 = (unsigned)__builtin_amdgcn_mov_dpp((int)w1, 0x4E, 0xf, 0xf, true);
           w0 = __builtin_amdgcn_perm(p0, w0, s2);
           w1 = __builtin_amdgcn_perm(p1, w1, s2);
           const unsigned s1 = (q & 1) ? 0x03070105u : 0x06020400u;
-          p0 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w0, 0xB1, 0xf, 0xf, false);  // lane ^ 1
-          p1 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0xB1, 0xf, 0xf, false);
+          p0 = (unsigned)__builtin_amdgcn_mov_dpp((int)w0, 0xB1, 0xf, 0xf, true);  // lane ^ 1
+          p1 = (unsigned)__builtin_amdgcn_mov_dpp((int)w1, 0xB1, 0xf, 0xf, true);
           qq_cur = make_uint2(__builtin_amdgcn_perm(p0, w0, s1), __builtin_amdgcn_perm(p1, w1, s1));
         }
       } else {
@@ -456,7 +486,7 @@ descriptor_kernel(DescArgs A) {
         advance();
         finish(loc_nxt, rc_nxt, odd_nxt);
       } else {
-        sample(base + 8 + q < nsamp, rc_nxt, odd_nxt);
+        locate(base + 8 + q < nsamp, loc_2);  // batch k + 1: finished after this batch's chain
       }
       // ordered accumulation of batch k: lane q applies its record of each sample
       if constexpr (PACKED) {
@@ -479,6 +509,13 @@ descriptor_kernel(DescArgs A) {
           const int a = (__float_as_int(e.x) << 6) + lane;
           hist[a] = hist[a] + e.y;
         }
+      }
+      if constexpr (PF == 1) {
+        // batch k + 1's gathered pixel is first used after the chain (an
+        // opaque copy behind the chain's LDS operations): its memory latency
+        // overlaps the chain whatever order the scheduler picks
+        asm volatile("" : "+v"(loc_2.mo_raw.x), "+v"(loc_2.mo_raw.y) : : "memory");
+        finish(loc_2, rc_nxt, odd_nxt);
       }
       wave_sync_d();
       if constexpr (PF == 2)
