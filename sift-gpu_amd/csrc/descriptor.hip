@@ -18,7 +18,8 @@
 //    per-lane LDS read-modify-writes, no atomics, no cross-lane hazards.  The
 //    histogram lives at [qidx][lane] (qidx = (R'>>1)*10 + (C'>>1)*5 + (O>>1)
 //    over the interior rows / columns R' = R-1, C' = C-1 in [0, 4) -- the only
-//    bins the fold reads; border-bin updates go to a trash row), so all 64
+//    bins the fold reads; a border-bin update goes to a trash row, or, in the
+//    packed form, carries +0.0 into an interior bin), so all 64
 //    lanes of an update hit distinct banks and a wave needs 5.4 KB, not
 //    11.5 KB (three waves per SIMD instead of two).
 //  * Fold, 0.2 clamp, uchar quantisation, RootSIFT (src/sift.cpp:676-721)
@@ -100,7 +101,7 @@ struct RecT {  // one lane's 8 corner records: (qidx, value) pairs
 template <>
 struct RecT<true> {
   float v[8];
-  unsigned qb[2];  // qidx of corner k in byte k & 3 of word k >> 2
+  unsigned qb[2];  // byte s (word s >> 2): qidx of corner s ^ odd, the one owner slot s takes
 };
 
 // DET: the keypoints come from this library's detection, so every window has
@@ -266,7 +267,8 @@ descriptor_kernel(DescArgs A) {
     // their parity bits, corner k = dr*4 + dc*2 + do lands in interior bin
     // (Rm+dr, Cm+dc, O0+do), whose parity -- its owner -- is k ^ odd, at
     //   qidx_k = qi0 + [dr and Rm odd]*10 + [dc and Cm odd]*5 + [do and O0 odd],
-    // or in the trash row when Rm+dr or Cm+dc leaves [0, 4).
+    // or outside the interior when Rm+dr or Cm+dc leaves [0, 4) (trash row;
+    // packed form: value +0.0).
     // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
     // the owner adds its lane to form the [qidx][lane] address.
     RecT<PACKED> rc_cur;  // (qidx, val) x 8 corners of this lane's sample
