@@ -1,19 +1,15 @@
 #!/bin/bash
-# One-image latency (tools/single_trace.py) of each lib/libsift_hip_<name>.so,
-# alternating, R rounds (default 3).
-# usage: tools/ab_single.sh <tag> <name>...
+# bench.py's one-image leg (configs[1]) with each lib/libsift_hip_<name>.so, alternating, R rounds.
 set -o pipefail
-TAG=$1; shift
+mkdir -p gpurun_out
 L=sift-gpu_amd/lib
-O=gpurun_out/single_$TAG
-mkdir -p $O
 cp $L/libsift_hip.so $L/libsift_hip_keep.so
-for r in $(seq ${R:-3}); do
-  for n in "$@"; do
-    cp $L/libsift_hip_$n.so $L/libsift_hip.so
-    echo -n "$n " >> $O/ab.txt
-    timeout -k 10 120 python3 tools/single_trace.py --reps 200 >> $O/ab.txt 2>> $O/stderr.txt || { echo "var $n failed"; tail -5 $O/ab.txt; cp $L/libsift_hip_keep.so $L/libsift_hip.so; exit 1; }
-  done
-done
+for r in $(seq ${R:-2}); do for n in "$@"; do
+  cp $L/libsift_hip_$n.so $L/libsift_hip.so
+  timeout -k 10 300 python3 bench.py --only single --steps 20 --warmup 5 > gpurun_out/abs_${n}_${r}.json 2>/dev/null || { cp $L/libsift_hip_keep.so $L/libsift_hip.so; exit 1; }
+  python3 -c "
+import json;d=json.loads(open('gpurun_out/abs_${n}_${r}.json').read().strip().splitlines()[-1])
+s=d.get('single_image') or {}
+print('$n', s.get('latency_ms'), s.get('device_no_graph_ms'), 'verified', s.get('output_verified'))"
+done; done
 cp $L/libsift_hip_keep.so $L/libsift_hip.so
-cat $O/ab.txt
