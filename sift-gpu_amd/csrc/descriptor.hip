@@ -498,11 +498,14 @@ descriptor_kernel(DescArgs A) {
         const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | (((g & 1) ^ 1) << 4)));
         const uint2 qq = qq_cur;
         const float vals[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+        // byte address qidx * 256 + lane * 4 in one v_perm_b32: byte 0 <- lane * 4
+        // (< 256), byte 1 <- the bin byte, bytes 2-3 <- 0 (selector 12)
+        const unsigned lane4 = (unsigned)lane << 2;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-          const int qi = ((jj < 4 ? qq.x : qq.y) >> (8 * (jj & 3))) & 0xff;
-          const int a = (qi << 6) + lane;
-          hist[a] = hist[a] + vals[jj];
+          const unsigned ab = __builtin_amdgcn_perm(lane4, jj < 4 ? qq.x : qq.y, 0x0c0c0004u | ((unsigned)(jj & 3) << 8));
+          float* hp = reinterpret_cast<float*>(reinterpret_cast<char*>(hist) + ab);
+          *hp = *hp + vals[jj];
         }
       } else {
 #pragma unroll
