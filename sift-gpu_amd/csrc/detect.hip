@@ -1495,9 +1495,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2
         const int i = si[u] - radius[u], j = sj[u] - radius[u];
         const bool okv = base + q < ns[u] && si[u] >= ilo[u] && si[u] <= ihi[u] && sj[u] >= jlo[u] &&
                          sj[u] <= jhi[u];
-        mo[u] = gwin[u][okv ? si[u] * pitch[u] + sj[u] : radius[u] * (pitch[u] + 1)];  // (Mag, Ori)
+        // 24-bit products, 32-bit offsets (full-rate VALU; a window's offsets are < 2^31)
+        mo[u] = gwin[u][(unsigned)(okv ? __mul24(si[u], pitch[u]) + sj[u] : __mul24(radius[u], pitch[u] + 1))];  // (Mag, Ori)
         // |argument| <= 2 * 17^2 / (2 * 2.85^2) < 36: exp32f's input clamp never acts
-        const float w = exp32f<false>((i * i + j * j) * escale[u], etab, ek);
+        const float w = exp32f<false>((__mul24(i, i) + __mul24(j, j)) * escale[u], etab, ek);
         wt[u] = okv ? w : -1.f;
         sj[u] += 8;  // D >= 19 > 8 for every kept candidate: at most one wrap
         if (sj[u] >= Dw[u]) {
