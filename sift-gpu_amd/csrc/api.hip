@@ -358,9 +358,9 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       launch_blur_plane(st, c->w_base, c->d_coef + c->coef_base_off, src, c->d_gpyr + L.oct[0].g_off[0],
                         L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
   }
-  // The 2-D tile and small-tile blurs also write the next octave's plane 0
-  // when it is an exact half (no decimation launch; the launches of one image
-  // are latency-bound); the scatter form leaves it to decimate_kernel.
+  // Every octave blur also writes the next octave's plane 0 when it is an
+  // exact half of plane 2 (no decimation launch; the launches of one image are
+  // latency-bound, and the batch's decimation was a full extra read of plane 2).
   bool fused = false;  // this octave's plane 0 came out of the previous launch
   for (int o = 0; o < L.n_oct; ++o) {
     const double px = plane_px(L, o) * batch;
@@ -372,10 +372,10 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       double taps = 0;
       for (int q = 0; q < 4; ++q) taps += (double)(2 * c->wsz[q] + 1) * (2 * c->wsz[q] + 1);
       const bool sym = use_sym_blur(c, L.oct[o].rows, L.oct[o].cols, batch);
-      const bool fuse = !sym && c->fuse_dec && o + 1 < L.n_oct && blur_fuses_decimation(L, o + 1);
+      const bool fuse = c->fuse_dec && o + 1 < L.n_oct && blur_fuses_decimation(L, o + 1);
       StageScope s(c, sym ? ST_BLUR_SYM : ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
       if (sym)
-        launch_blur_octave_sym(st, L, o, c->d_gpyr, batch);
+        launch_blur_octave_sym(st, L, o, c->d_gpyr, batch, fuse);
       else if (blur_octave_tiles(L, o, batch) < c->small_max)
         launch_blur_octave_small(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch, fuse);
       else

@@ -495,6 +495,8 @@ struct SymArgs {
   long long s_pitch, s_img;
   float* dst[4];       // per slot, image 0
   long long d_pitch, d_img;
+  float* nxt;          // the next octave's plane 0 (image 0) when it is plane 2's exact half, else null
+  long long n_pitch;
   int rows, cols, strips, batch;
   int start[5];        // first wave of each slot; start[nslot] = grid size
   int chunk[4];        // output rows per wave, per slot
@@ -584,7 +586,14 @@ __device__ __forceinline__ void sym_walk(const SymArgs& A, int slot, int local, 
         }
       }
       const int y = r - W;  // complete: its last kernel row was r
-      if (y >= y0 && y < y1 && xo < cols) dst[(long long)y * A.d_pitch + xo] = acc[i] / 8192.f;
+      if (y >= y0 && y < y1 && xo < cols) {
+        const float v = acc[i] / 8192.f;
+        dst[(long long)y * A.d_pitch + xo] = v;
+        // plane nOctaveLayers (slot 2) -> the next octave's plane 0, INTER_NEAREST
+        // exact half (src/sift.cpp:252-254): pixel (2y', 2x') -> (y', x')
+        if constexpr (T == 2)
+          if (A.nxt && ((y | xo) & 1) == 0) A.nxt[b * A.d_img + (long long)(y >> 1) * A.n_pitch + (xo >> 1)] = v;
+      }
     }
 #pragma unroll
     for (int k = 0; k < NA - R; ++k) acc[k] = acc[k + R];
@@ -707,9 +716,12 @@ void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitc
   hipLaunchKernelGGL(blur_sym_base_kernel, dim3(A.start[1]), dim3(64), 0, st, A);
 }
 
-void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch) {
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next) {
   const Octave& O = L.oct[o];
   SymArgs A{};
+  const NextPlane nx = next_plane(L, o, gpyr, fuse_next);
+  A.nxt = nx.p;
+  A.n_pitch = nx.pitch;
   A.src = gpyr + O.g_off[0];
   A.s_pitch = O.pitch;
   A.s_img = L.g_img;

@@ -221,7 +221,7 @@ long long blur_octave_tiles(const Layout& L, int o, int batch);
 bool sym_tables_match(const float* coefs);
 void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitch, long long dimg, int rows,
                           int cols, int batch);
-void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch);
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next);
 void launch_decimate(hipStream_t st, const Layout& L, int o, float* gpyr, int batch);
 void launch_dog(hipStream_t st, const Layout& L, int o, const float* gpyr, float* dog, int batch);
 void launch_blur_1d(hipStream_t st, int w, const float* coef1d, Plane src, float* tmp, float* dst,
