@@ -32,7 +32,9 @@
 #include <type_traits>
 
 // waves per SIMD the batch descriptor kernel is compiled for (register budget;
-// 3 with no spills measured 8.4-8.5 vs 7.6 ms, round 3)
+// 3 with no spills measured 8.4-8.5 vs 7.6 ms, round 3; 5 -- 96 VGPRs, spills
+// outside the sample loop -- 8.34 vs 6.42-6.46 ms, round 4,
+// profiles/r4_desc_wpe5_ab.txt)
 constexpr int kDescWpe = 4;
 
 namespace sift {
@@ -107,22 +109,28 @@ struct RecT<true> {
 // DET: the keypoints come from this library's detection, so every window has
 // radius <= 40 (scl < 1.6 * 2^1.25, src/sift.cpp:588) and a row table: the
 // whole-window walk and its interior tests compile away.
-// PF: sample batches in flight.  1: the next batch's gather is issued and
-// used in the step that runs this batch's chain (default: with many waves per
-// SIMD the gather latency hides behind other waves).  2 (launches of one
-// image, round 3): its gather is issued a step earlier, so a wave that is
-// alone on its SIMD does not wait a full memory latency per batch.
-template <bool PACKED, bool DET, int PF = 1>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PF == 2 ? 2 : PACKED ? kDescWpe : 1))) void
+// PF: sample batches in flight.  1: the next batch's gather is issued in the
+// step that runs this batch's chain and used right after it.  2 (default for
+// detected keypoints): its gather is issued a step earlier, so it flies for a
+// whole step -- a wave that is alone on its SIMD (one image) no longer waits a
+// full memory latency per batch, and at four waves per SIMD (batches) the
+// descriptor took 6.36-6.38 vs 6.49-6.54 ms per 64 x 1080p step
+// (profiles/r4_desc_pf2_ab.txt).  WPE: waves per SIMD the registers are
+// budgeted for (PF = 2 at 4: 128 VGPRs, the spills outside the sample loop).
+template <bool PACKED, bool DET, int PF, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 descriptor_kernel(DescArgs A) {
-  __shared__ float hist[kQBins * 64];               // [qidx][group*8 + parity]
-  // per-sample hand-off records (see RecT)
+  // [qidx][group*8 + parity]; the packed form has no trash row
+  constexpr int kHistRows = PACKED ? kQBins - 1 : kQBins;
+  __shared__ float hist[kHistRows * 64];
+  // per-sample hand-off records (see RecT); outside the sample loop the same
+  // words hold the sub-batch's keypoint indices and the normalisation scalars
   __shared__ __attribute__((aligned(16))) float rec[PACKED ? kGrp * kRecG : 8 * kRecStride2];
   // per row: (jlo + 64) | len << 16 (PACKED: << 8, 16 bits)
   __shared__ typename std::conditional<PACKED, unsigned short, int>::type rows_tab[kGrp][kMaxWinRows];
   constexpr int kLenSh = PACKED ? 8 : 16, kLoMask = PACKED ? 0xff : 0xffff;
-  __shared__ float bc[kGrp][4];
-  __shared__ int sord[kGrp];                        // this sub-batch's keypoint indices
+  int* const sord = reinterpret_cast<int*>(rec);                 // [kGrp] keypoint indices
+  float(*const bc)[4] = reinterpret_cast<float(*)[4]>(rec + kGrp);  // [kGrp][4] normalisation scalars
   const int lane = threadIdx.x & 63;
   const int g = lane >> 3, q = lane & 7;
   const int d = kDescW, nb = kDescBins;
@@ -234,7 +242,7 @@ descriptor_kernel(DescArgs A) {
     } else {
       nsamp = D * D;  // radius > 40 (caller-supplied keypoints): the whole window
     }
-    for (int t = 0; t < kQBins; ++t) hist[t * 64 + lane] = 0.f;
+    for (int t = 0; t < kHistRows; ++t) hist[t * 64 + lane] = 0.f;
     int nmax = nsamp;
     nmax = max(nmax, __shfl_xor(nmax, 8));
     nmax = max(nmax, __shfl_xor(nmax, 16));
@@ -639,28 +647,27 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
     const char* e = getenv("SIFT_HIP_DESC_PACKED");  // A/B switch between the two record forms
     return !e || atoi(e) != 0;
   }();
-  // one image per call (the single-image path): few waves, latency-bound
-  // chains -- gathers two batches ahead (SIFT_HIP_DESC_DEEP=0/1 overrides)
-  static const int deep_env = [] {
+  // detected keypoints gather two batches ahead (PF = 2): one image per call
+  // is budgeted for 2 waves per SIMD (few waves, latency-bound chains),
+  // batches for kDescWpe; SIFT_HIP_DESC_DEEP=0 selects the one-ahead form
+  static const bool deep = [] {
     const char* e = getenv("SIFT_HIP_DESC_DEEP");
-    return e ? atoi(e) : -1;
+    return !e || atoi(e) != 0;
   }();
-  const bool deep = deep_env >= 0 ? deep_env != 0 : batch == 1;
-  if (packed && detected && deep)
-    hipLaunchKernelGGL((descriptor_kernel<true, true, 2>),
-                       dim3(resident_grid((const void*)descriptor_kernel<true, true, 2>, 64, 0, 8192)), dim3(64), 0, st,
-                       A);
+#define SIFT_DESC_LAUNCH(...)                                                                                       \
+  hipLaunchKernelGGL((descriptor_kernel<__VA_ARGS__>),                                                              \
+                     dim3(resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192)), dim3(64), 0, st, A)
+  if (packed && detected && deep && batch == 1)
+    SIFT_DESC_LAUNCH(true, true, 2, 2);
+  else if (packed && detected && deep)
+    SIFT_DESC_LAUNCH(true, true, 2, kDescWpe);
   else if (packed && detected)
-    hipLaunchKernelGGL((descriptor_kernel<true, true>),
-                       dim3(resident_grid((const void*)descriptor_kernel<true, true>, 64, 0, 8192)), dim3(64), 0, st, A);
+    SIFT_DESC_LAUNCH(true, true, 1, kDescWpe);
   else if (packed)
-    hipLaunchKernelGGL((descriptor_kernel<true, false>),
-                       dim3(resident_grid((const void*)descriptor_kernel<true, false>, 64, 0, 8192)), dim3(64), 0, st,
-                       A);
+    SIFT_DESC_LAUNCH(true, false, 1, kDescWpe);
   else
-    hipLaunchKernelGGL((descriptor_kernel<false, false>),
-                       dim3(resident_grid((const void*)descriptor_kernel<false, false>, 64, 0, 8192)), dim3(64), 0,
-                       st, A);
+    SIFT_DESC_LAUNCH(false, false, 1, 1);
+#undef SIFT_DESC_LAUNCH
 }
 
 }  // namespace sift
