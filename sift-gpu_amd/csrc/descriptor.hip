@@ -412,21 +412,19 @@ descriptor_kernel(DescArgs A) {
         rlo = mv ? (enext & kLoMask) - 64 : rlo;
         rlen = mv ? enext >> kLenSh : rlen;
       }
-      if (__builtin_amdgcn_ballot_w64(ri < D && u >= rlen) != 0) {
-        while (ri < D && u >= rlen) {
-          u -= rlen;
-          if (++ri < D && table) {
-            const int e = rows_tab[g][ri];
-            rlo = (e & kLoMask) - 64;
-            rlen = e >> kLenSh;
-          }
+      while (ri < D && u >= rlen) {  // skipped by exec when no lane needs it
+        u -= rlen;
+        if (++ri < D && table) {
+          const int e = rows_tab[g][ri];
+          rlo = (e & kLoMask) - 64;
+          rlen = e >> kLenSh;
         }
       }
       enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
     };
     int odd_cur = 0;
     uint2 qq_cur = make_uint2(0u, 0u);  // PACKED: this owner's 8 bin bytes of the batch
-    Loc loc_nxt;  // PF = 2: batch k + 1, located and gathering
+    Loc loc_nxt, loc_alt;  // PF = 2: batches k + 1 and k + 2, located and gathering (two buffers)
     if (nmax > 0) {
       if constexpr (PF == 2) {
         Loc l0;
@@ -440,7 +438,9 @@ descriptor_kernel(DescArgs A) {
         advance();
       }
     }
-    for (int base = 0; base < nmax; base += 8) {
+    // one batch: ln = batch k + 1 (PF = 2; located a step ago), l2 = the batch
+    // located in this step
+    auto step = [&](int base, Loc& ln, Loc& l2) {
       if constexpr (PACKED) {
         // corner k to owner slot s = k ^ odd: value at byte (g << 8) | (s << 5) |
         // (q << 2), bit 4 flipped on odd groups (so a 16-lane pass of the
@@ -490,13 +490,12 @@ descriptor_kernel(DescArgs A) {
       wave_sync_d();
       RecT<PACKED> rc_nxt;
       int odd_nxt = 0;
-      Loc loc_2;
       if constexpr (PF == 2) {
-        locate(base + 16 + q < nsamp, loc_2);  // batch k + 2: its gather flies for a whole step
+        locate(base + 16 + q < nsamp, l2);  // batch k + 2: its gather flies for two steps
         advance();
-        finish(loc_nxt, rc_nxt, odd_nxt);
+        finish(ln, rc_nxt, odd_nxt);
       } else {
-        locate(base + 8 + q < nsamp, loc_2);  // batch k + 1: finished after this batch's chain
+        locate(base + 8 + q < nsamp, l2);  // batch k + 1: finished after this batch's chain
       }
       // ordered accumulation of batch k: lane q applies its record of each sample
       if constexpr (PACKED) {
@@ -527,16 +526,24 @@ descriptor_kernel(DescArgs A) {
         // batch k + 1's gathered pixel is first used after the chain (an
         // opaque copy behind the chain's LDS operations): its memory latency
         // overlaps the chain whatever order the scheduler picks
-        asm volatile("" : "+v"(loc_2.mo_raw.x), "+v"(loc_2.mo_raw.y) : : "memory");
-        finish(loc_2, rc_nxt, odd_nxt);
+        asm volatile("" : "+v"(l2.mo_raw.x), "+v"(l2.mo_raw.y) : : "memory");
+        finish(l2, rc_nxt, odd_nxt);
       }
       wave_sync_d();
-      if constexpr (PF == 2)
-        loc_nxt = loc_2;
-      else
-        advance();
+      if constexpr (PF == 1) advance();
       rc_cur = rc_nxt;
       odd_cur = odd_nxt;
+    };
+    if constexpr (PF == 2) {
+      // unrolled by two so the two Loc buffers swap roles instead of being
+      // copied (a copy of the gathered pixel would wait for its load)
+      for (int base = 0; base < nmax; base += 16) {
+        step(base, loc_nxt, loc_alt);
+        if (base + 8 >= nmax) break;
+        step(base + 8, loc_alt, loc_nxt);
+      }
+    } else {
+      for (int base = 0; base < nmax; base += 8) step(base, loc_nxt, loc_alt);
     }
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
     float cell[2][8];

@@ -67,20 +67,27 @@ def check_kernel(name, lines):
         return errs, len(seq) // 8
     slots = None
     for n, (mi, k) in enumerate(marks):
-        # the opaque copy: the register the marker's asm holds ("+v"), set by
-        # the v_mov right before it
-        prev = [l for i, l in code if i < mi and not l.startswith(';')]
-        mov = next((l for l in reversed(prev[-4:]) if l.startswith('v_mov_b32')), None)
-        if mov is None:
-            errs.append(f'{name}: step {k}: no opaque lane copy before the marker')
-            continue
-        copy_reg = mov.split()[1].rstrip(',')
+        # the opaque copy: the register the marker's asm holds ("+v"), which
+        # the guard compares; its last write before the marker must be the
+        # v_mov that copies the lane index (the scheduler may hoist it)
         nxt = marks[n + 1][0] if n + 1 < len(marks) else len(lines)
         seg = [l for i, l in code if mi < i < nxt and l and not l.startswith(';') and not l.startswith('.')]
         cmp_i = next((j for j, l in enumerate(seg) if l.startswith('v_cmp_eq_u32')), None)
-        if cmp_i is None or not re.search(rf'\b{k}, {copy_reg}\b', seg[cmp_i]):
-            errs.append(f'{name}: step {k}: guard is not v_cmp_eq_u32 {k}, {copy_reg} '
+        m_cmp = re.search(rf'\b{k}, (v\d+)$', seg[cmp_i]) if cmp_i is not None else None
+        if m_cmp is None:
+            errs.append(f'{name}: step {k}: guard is not v_cmp_eq_u32 {k}, <lane copy> '
                         f'({seg[cmp_i] if cmp_i is not None else "missing"})')
+            continue
+        copy_reg = m_cmp.group(1)
+        prev = [l for i, l in code if i < mi and l and not l.startswith(';') and not l.startswith('.')]
+        writer = next((l for l in reversed(prev) if l.split()[0].startswith('v_') and len(l.split()) > 1 and
+                       l.split()[1].rstrip(',') == copy_reg), None)
+        if writer is None or not writer.startswith('v_mov_b32'):
+            errs.append(f'{name}: step {k}: {copy_reg} is not an opaque lane copy ({writer})')
+            continue
+        if any(re.search(rf'\b{copy_reg}\b', l) and l.split()[1].rstrip(',') == copy_reg
+               for l in seg[:cmp_i] if len(l.split()) > 1):
+            errs.append(f'{name}: step {k}: {copy_reg} rewritten between the marker and the guard')
             continue
         sv = next((j for j in range(cmp_i, len(seg)) if seg[j].startswith('s_and_saveexec')), None)
         end = next((j for j in range(sv or 0, len(seg)) if seg[j].startswith('s_or_b64 exec')), None)
