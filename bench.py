@@ -25,8 +25,13 @@ single-image latency (hipGraph replay, 4 octaves), configs[4] (one 8K image,
 output checked, pyramid rooflines at C5), the knnMatch leg, and the CPU
 baseline (oracle, 1 thread + image-parallel on the host's cores).
 
-Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU, RCCL).  Rank 0 prints one JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W].  At N > 1 without a
+launcher, bench.py starts `python -m torch.distributed.run --nproc-per-node N
+--master-addr 127.0.0.1 ... bench.py <same args>` as a child process (one rank
+per GPU, RCCL) and exits with its code; under a launcher WORLD_SIZE must equal
+--gpus.  Rank 0 prints one JSON line.  Exit codes: 0 ok; 3 a device (HIP)
+error was caught in an optional leg; 4 the headline's output check failed
+(the line is printed first in both cases).
 """
 from __future__ import annotations
 
@@ -441,6 +446,20 @@ def match_cpu_baseline(m, n_sample=64):
             "gpu_equals_oracle_on_sample": same}
 
 
+def is_gpu_error(e) -> bool:
+    """A device-side failure: the library's HIP error code, or torch's
+    accelerator error (a HIP runtime error raised by torch)."""
+    if isinstance(e, siftgpu.SiftError) and e.code == siftgpu.SIFT_E_HIP:
+        return True
+    acc = getattr(torch, "AcceleratorError", None)
+    if acc is not None and isinstance(e, acc):
+        return True
+    return isinstance(e, RuntimeError) and str(e).startswith(("HIP error", "CUDA error"))
+
+
+GPU_ERROR_LEGS = set()   # legs whose caught exception was a device-side failure
+
+
 def guarded(errors, name, fn, *args, **kw):
     """Runs one optional leg; a failure is recorded as errors[name] and the
     leg's block as {"error": ...} instead of costing the headline line."""
@@ -448,6 +467,8 @@ def guarded(errors, name, fn, *args, **kw):
         return fn(*args, **kw)
     except Exception as e:  # noqa: BLE001 -- any failure of an optional leg
         errors[name] = f"{type(e).__name__}: {e}"[:400]
+        if is_gpu_error(e):
+            GPU_ERROR_LEGS.add(name)
         print(f"bench.py: leg {name} failed: {errors[name]}", file=sys.stderr, flush=True)
         return None
 
@@ -694,6 +715,9 @@ def exact_block(a, world, B, R, C, S, res, tr):
     pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
     gathering = res.get("gather") is not None
     out.update({
+        # first after the metric: the driver's record keeps only the line's head
+        "output_verified": bool(verified) and not failed,
+        "output_verified_seeds": verified,
         "value": round(value, 2),
         "unit": "Mpix/s",
         "n_gpus": world,
@@ -711,8 +735,6 @@ def exact_block(a, world, B, R, C, S, res, tr):
                    "mode": "exact (bit-identical to the CPU path)",
                    "parallelism": f"image-sharded x{world}, {S} HIP streams x {B // S} images per GPU" +
                                   (", RCCL keypoint gather one step behind" if gathering else "")},
-        "output_verified": bool(verified) and not failed,
-        "output_verified_seeds": verified,
         "keypoints_per_s": round(kp_total_step * a.steps / dt, 1),
         "keypoints_per_step": int(kp_total_step),
         "roofline": roof,
@@ -833,8 +855,54 @@ def assemble(a, world, env_shape, res, cpu, errors):
     return out
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv=None) -> int:
+    """`--gpus N > 1` without a launcher: run N ranks of this script under
+    torch.distributed.run as a CHILD process (never an exec: nothing here has
+    touched the GPU, and the child's ranks initialise their own devices), one
+    rank per GPU, rendezvous on 127.0.0.1.  Rank 0's line reaches our stdout
+    through the inherited descriptor; returns the child's exit code."""
+    argv = sys.argv[1:] if argv is None else argv
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    print(f"bench.py: launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(a):
+    """The rank count the launcher gave us must be the one --gpus asks for,
+    and the node must have that many devices (device_count does not
+    initialise the GPU on this image).  Returns an error message or None."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and world != a.gpus:
+        return f"WORLD_SIZE={world} but --gpus {a.gpus}: launch one rank per requested GPU"
+    if a.gpus > 1:
+        n = torch.cuda.device_count()
+        if a.gpus > n:
+            return f"--gpus {a.gpus} but only {n} HIP device(s) visible"
+    return None
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        n = torch.cuda.device_count()
+        if a.gpus > n:
+            sys.exit(f"bench.py: --gpus {a.gpus} but only {n} HIP device(s) visible")
+        sys.exit(launch_ranks(a))
+    GPU_ERROR_LEGS.clear()
+    msg = check_world(a)
+    if msg:
+        sys.exit(f"bench.py: {msg}")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -865,19 +933,39 @@ def main():
         res["single"] = guarded(errors, "single", single_image_leg, env.R, env.C, a.steps, a.warmup)
     if rank == 0 and world == 1 and not a.no_8k and want("8k"):
         res["eightk"] = guarded(errors, "eightk", eightk_leg, a.steps, a.warmup)
+    verified_ok = True
     if rank == 0:
         out = assemble(a, world, (env.B, env.R, env.C, env.S), res, cpu, errors)
+        out["distributed"] = {"world_size": world, "backend": dist.get_backend() if world > 1 else None,
+                              "launcher": "torch.distributed.run" if "WORLD_SIZE" in os.environ else "none"}
         if a.profile_json and res.get("exact") is not None:
             with open(a.profile_json, "w") as f:
                 json.dump(res["exact"]["prof"][1], f, indent=1)
         print(json.dumps(out), flush=True)
+        verified_ok = output_check_passed(a, out, res)
     env.close()
     if world > 1:
         dist.destroy_process_group()
     # a GPU error caught in an optional leg leaves the line printed but the
     # run marked failed: the context that raised it is not trusted further
-    if any(("hip" in v.lower() or "HIP" in v) for v in errors.values()):
+    if GPU_ERROR_LEGS:
         sys.exit(3)
+    if not verified_ok:
+        print("bench.py: output check failed (output_verified false or a seed differs from the CPU path's "
+              "digests)", file=sys.stderr, flush=True)
+        sys.exit(4)
+
+
+def output_check_passed(a, out, res) -> bool:
+    """The headline's output check must pass for the run to pass: at the
+    golden shape every checked seed must equal the CPU path's digest (count,
+    keypoint bytes, descriptor bytes) and none may fail.  Shapes without
+    digests (--rows/--cols/--octaves changed) are not checked."""
+    if res.get("exact") is None:
+        return True
+    if a.octaves != 5 or (a.rows, a.cols) != (1080, 1920):
+        return True
+    return bool(out.get("output_verified")) and not out.get("output_failed_seeds")
 
 
 if __name__ == "__main__":

@@ -129,6 +129,7 @@ struct sift_ctx {
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
   bool fast_ok = false;           // SIFT_FLAG_FAST: pyramid_tri.hip's compiled-in taps equal the host's
   bool fuse_dec = true;           // 2-D tile blurs write the next plane 0 (SIFT_HIP_FUSE_DEC=0: decimate_kernel)
+  bool poison_pad = false;        // test switch SIFT_HIP_POISON_PAD=1: NaN into every plane's pitch padding
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
   long long small_max = 2048;
@@ -320,6 +321,43 @@ bool use_sym_blur(const sift_ctx* c, int rows, int cols, int batch) {
   return c->sym_blur && rows >= c->sym_rows && (long long)((cols + 63) / 64) * batch >= c->sym_min;
 }
 
+// Test switch for the pitch-padding invariant (common.hpp, kPitchAlign):
+// overwrite columns [cols, pitch) of every Gaussian plane of the batch with a
+// NaN once the pyramid is built, so a later kernel that read them would change
+// its output (tests/test_gpu_fast.py::test_pitch_padding_is_never_read).
+struct PadArgs {
+  float* gpyr;
+  long long g_img;
+  int n_planes;
+  long long off[kMaxOctaves * kScales];
+  int rows[kMaxOctaves * kScales], cols[kMaxOctaves * kScales], pitch[kMaxOctaves * kScales];
+};
+__global__ __launch_bounds__(64) void poison_pad_kernel(PadArgs A) {
+  int r = blockIdx.x, p = 0;
+  while (p < A.n_planes && r >= A.rows[p]) r -= A.rows[p++];
+  if (p >= A.n_planes) return;
+  const int x = A.cols[p] + (int)threadIdx.x;
+  if (x < A.pitch[p])
+    A.gpyr[(long long)blockIdx.y * A.g_img + A.off[p] + (long long)r * A.pitch[p] + x] = __builtin_nanf("");
+}
+void enqueue_poison_pad(sift_ctx* c, const Layout& L, int batch) {
+  PadArgs A{};
+  A.gpyr = c->d_gpyr;
+  A.g_img = L.g_img;
+  int total = 0;
+  for (int o = 0; o < L.n_oct; ++o)
+    for (int s = 0; s < kScales; ++s) {
+      const int p = A.n_planes++;
+      A.off[p] = L.oct[o].g_off[s];
+      A.rows[p] = L.oct[o].rows;
+      A.cols[p] = L.oct[o].cols;
+      A.pitch[p] = L.oct[o].pitch;
+      total += L.oct[o].rows;
+    }
+  static_assert(kPitchAlign <= 64, "one lane per padding column");
+  hipLaunchKernelGGL(poison_pad_kernel, dim3(total, batch), dim3(64), 0, c->stream, A);
+}
+
 // Gaussian pyramid (src/sift.cpp:229-263) + DoG (:265-283) for a batch whose
 // input planes are described by src.  Async on c->stream.
 void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool with_dog) {
@@ -341,6 +379,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
       launch_pyramid_tri(st, L, o, c->d_gpyr, src, batch);
     }
+    if (c->poison_pad) enqueue_poison_pad(c, L, batch);
     if (with_dog)
       for (int o = 0; o < L.n_oct; ++o) {
         StageScope s(c, ST_DOG, 4.0 * plane_px(L, o) * batch, 36.0 * plane_px(L, o) * batch);
@@ -387,6 +426,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       launch_dog(st, L, o, c->d_gpyr, c->d_dog, batch);
     }
   }
+  if (c->poison_pad) enqueue_poison_pad(c, L, batch);
 }
 
 // dog_from_gpyr: the fused extrema pass forms the DoG values from the Gaussian
@@ -708,6 +748,8 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   {
     const char* fd = getenv("SIFT_HIP_FUSE_DEC");
     c->fuse_dec = !(fd && atoi(fd) == 0);
+    const char* pp = getenv("SIFT_HIP_POISON_PAD");
+    c->poison_pad = pp && atoi(pp) != 0;
   }
   MathConsts mc;
   host_math_consts(&mc);

@@ -37,6 +37,13 @@ constexpr double kCvPi = 3.1415926535897932384626433832795;
 // boundary: a 64-column strip's row is two whole lines, never a partial-line
 // write.  (With 64-B pitches the 1080p image block was 55,251,520 B, an odd
 // number of half lines, so every odd image of a batch was misaligned.)
+// Invariant: the pitch padding columns [cols, pitch) of every plane hold
+// unspecified values.  SIFT_FLAG_FAST's dwordx4 / dwordx2 plane stores
+// (pyramid_tri.hip) write whole 4-column groups past cols there, and no kernel
+// reads a column >= cols of a Gaussian or DoG plane (every reader bounds its
+// columns by cols, and the sub-module API copies planes out row by row with
+// cols columns); tests/test_gpu_fast.py::test_fast_ignores_pitch_padding
+// poisons the padding with NaN and requires unchanged results.
 constexpr int kPitchAlign = 32;
 struct Octave {
   int rows, cols, pitch;
@@ -191,8 +198,8 @@ void host_math_consts(MathConsts* mc);
 // once runs in rounds, and the last, partial round idles the rest of the chip
 // (8192 orientation waves on 6144 wave slots = 2 rounds for 1.33 rounds of
 // work).  So the grid is the resident count: occupancy API x CUs, a multiple
-// of 8 (the kernels' XCD split), cached per kernel.  SIFT_HIP_FIXED_GRID=1
-// restores the fixed grid (A/B runs).
+// of 8 (the kernels' XCD split), cached per kernel; fixed_grid is the
+// fallback when the occupancy query fails.
 int resident_grid(const void* kernel, int block, size_t lds, int fixed_grid);
 
 // ---- host launchers (defined in the .hip files) --------------------------

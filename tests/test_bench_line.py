@@ -77,6 +77,117 @@ def test_line_survives_failing_cpu_leg(bench, monkeypatch, capsys):
     assert "cpu_baseline_gpu_share" not in out and "cpu leg hung" in out["leg_errors"]["cpu_baseline_gpu_share"]
 
 
+def _quiet_legs(B, monkeypatch):
+    for leg in ("run_fast", "run_match", "single_image_leg", "eightk_leg"):
+        monkeypatch.setattr(B, leg, lambda *a, **k: None)
+
+
+def test_gpus_n_launches_ranks_as_child(bench, monkeypatch):
+    """--gpus N > 1 without WORLD_SIZE: torch.distributed.run as a child
+    process with the same arguments; its exit code is ours (VERDICT r4 #1)."""
+    import torch
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, **kw):
+        seen["cmd"] = cmd
+        return Done()
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(bench, "Env", lambda *a, **k: pytest.fail("the launcher touched the GPU"))
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "3", "--warmup", "1"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 7
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
+    assert any(c.startswith("--master-port=") and int(c.split("=")[1]) > 0 for c in cmd)
+    i = [k for k, c in enumerate(cmd) if c.endswith("bench.py")][0]
+    assert cmd[i + 1:] == ["--gpus", "8", "--steps", "3", "--warmup", "1"]
+
+
+def test_gpus_mismatch_fails(bench, monkeypatch):
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code not in (0, None) and "WORLD_SIZE=2" in str(ex.value.code)
+
+
+def test_gpus_more_than_devices_fails(bench, monkeypatch):
+    import torch
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setattr(bench.subprocess, "run", lambda *a, **k: pytest.fail("launched with too few devices"))
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code not in (0, None) and "only 1" in str(ex.value.code)
+
+
+def test_line_carries_world_and_launcher(bench, monkeypatch, capsys):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    _quiet_legs(bench, monkeypatch)
+    out = _run(bench, monkeypatch, capsys, ["--no-cpu-baseline"])
+    assert out["distributed"] == {"world_size": 1, "backend": None, "launcher": "none"}
+    keys = list(out)
+    assert keys.index("output_verified") < keys.index("value") < 4
+
+
+def test_failed_output_check_fails_the_run(bench, monkeypatch, capsys):
+    """VERDICT r4 #4: the line is printed, then rc != 0."""
+    _quiet_legs(bench, monkeypatch)
+    monkeypatch.setattr(bench, "run_exact", lambda env: {"exact": (0.1, {}, 800000.0),
+                                                         "prof": (0.12, _stats(), 0.0),
+                                                         "verified": [0, 63], "failed": [31], "gather": None})
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--no-cpu-baseline"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 4
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")]
+    out = json.loads(lines[0])
+    assert out["output_verified"] is False and out["output_failed_seeds"] == [31]
+
+
+def test_unverified_without_failures_fails_the_run(bench, monkeypatch, capsys):
+    _quiet_legs(bench, monkeypatch)
+    monkeypatch.setattr(bench, "run_exact", lambda env: {"exact": (0.1, {}, 800000.0),
+                                                         "prof": (0.12, _stats(), 0.0),
+                                                         "verified": [], "failed": [], "gather": None})
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--no-cpu-baseline"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 4
+
+
+def test_gpu_error_flag_by_exception_type(bench, monkeypatch, capsys):
+    """ADVICE r4: exit 3 on a device error only, not on any message holding
+    the letters 'hip' (a 'chip' in a CPU leg's message must not count)."""
+    import siftgpu
+    monkeypatch.setattr(bench, "GPU_ERROR_LEGS", set())
+    _quiet_legs(bench, monkeypatch)
+
+    def chip(*a, **k):
+        raise RuntimeError("relationship with the chip went wrong")
+    monkeypatch.setattr(bench, "single_image_leg", chip)
+    out = _run(bench, monkeypatch, capsys, ["--no-cpu-baseline"])
+    assert "chip" in out["leg_errors"]["single"]
+
+    def hip(*a, **k):
+        raise siftgpu.SiftError("sift_sync", siftgpu.SIFT_E_HIP, "illegal address")
+    monkeypatch.setattr(bench, "single_image_leg", hip)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--no-cpu-baseline"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 3
+
+
 def test_line_survives_failing_block(bench, monkeypatch, capsys):
     """A leg that returns but whose block cannot be built (missing stage)."""
     monkeypatch.setattr(bench, "run_fast", lambda env: ((0.05, {}, 1.0), None))

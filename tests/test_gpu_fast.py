@@ -187,6 +187,29 @@ def test_fast_batch_equals_single(fctx, oracle, B, R, C):
         assert dd[o[b]:o[b + 1]].tobytes() == ds.tobytes()
 
 
+@pytest.mark.parametrize("flags", [0, FAST])
+@pytest.mark.parametrize("shape,b", [((203, 157), 2), ((540, 960), 5), ((257, 4100), 7)])
+def test_pitch_padding_is_never_read(siftgpu, oracle, monkeypatch, flags, shape, b):
+    """the fast pyramid's wide stores leave unspecified values in
+    the pitch padding (common.hpp, kPitchAlign).  With SIFT_HIP_POISON_PAD=1
+    the library writes a NaN into every padding column of every plane after
+    the pyramid; the detect + describe output must not change, in fast and
+    exact mode (shapes with padding at every octave)."""
+    img = oracle.synth_image(b, *shape)
+    out = []
+    for poison in ("0", "1"):
+        monkeypatch.setenv("SIFT_HIP_POISON_PAD", poison)   # read at context creation
+        ctx = siftgpu.Context(*shape, 1, device=0, flags=flags)
+        try:
+            out.append(ctx.SIFT_NCL(img))
+        finally:
+            ctx.close()
+    (k0, d0), (k1, d1) = out
+    assert len(k0) > 10
+    assert np.ascontiguousarray(k0).tobytes() == np.ascontiguousarray(k1).tobytes()
+    assert d0.tobytes() == d1.tobytes()
+
+
 def test_fast_headline_batch_equals_single(siftgpu):
     """configs[2] in fast mode: one 64 x 1080p batch call (other chunk seams
     than a single image's launch) gives images 0, 31 and 63 bit-identical to

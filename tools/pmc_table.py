@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch counter table from rocprofv3 --pmc passes (tools/pmc_tri.sh).
+"""Per-launch counter table from rocprofv3 --pmc passes (tools/pmc.sh).
 
   python tools/pmc_table.py gpurun_out/pmc_<tag>
 

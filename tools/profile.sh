@@ -8,7 +8,7 @@
 #   cal_f/cal_w  the same counters over tools/fetch_calib (known byte counts)
 #   sqA..sqC   SQ / GRBM / TCC counter groups over tools/stage_bench.py for the
 #              named kernels (exact path), sqF* the same for pyr_tri_kernel (SIFT_FLAG_FAST default)
-# usage: tools/profile_r3.sh <tag> [bench args...]
+# usage: tools/profile.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r2}; shift
 OUT=gpurun_out/prof_$TAG

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile_r2.sh run into profiles/<tag>_*.
+"""Summarise a tools/profile.sh run into profiles/<tag>_*.
 
   python tools/rocprof_summary.py <tag>   (reads gpurun_out/prof_<tag>/)
 
