@@ -130,6 +130,8 @@ struct sift_ctx {
   bool fast_ok = false;           // SIFT_FLAG_FAST: pyramid_tri.hip's compiled-in taps equal the host's
   bool fuse_dec = true;           // 2-D tile blurs write the next plane 0 (SIFT_HIP_FUSE_DEC=0: decimate_kernel)
   bool poison_pad = false;        // test switch SIFT_HIP_POISON_PAD=1: NaN into every plane's pitch padding
+  bool pyr_tri = false;
+  bool sym_xcd = false;           // scatter blur in XCD-contiguous wave order (SIFT_HIP_SYM_XCD=1, A/B)           // SIFT_FLAG_FAST on pyramid_tri.hip (SIFT_HIP_PYR_TRI=1) instead of pyramid_pc.hip
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
   long long small_max = 2048;
@@ -377,7 +379,10 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
         launch_decimate(st, L, o, c->d_gpyr, batch);
       }
       StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-      launch_pyramid_tri(st, L, o, c->d_gpyr, src, batch);
+      if (c->pyr_tri)
+        launch_pyramid_tri(st, L, o, c->d_gpyr, src, batch);
+      else
+        launch_pyramid_pc(st, L, o, c->d_gpyr, src, batch, c->d_err + 3);
     }
     if (c->poison_pad) enqueue_poison_pad(c, L, batch);
     if (with_dog)
@@ -392,7 +397,8 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
     const int k = 2 * c->w_base + 1;
     StageScope s(c, ST_BLUR_BASE, 2.0 * k * k * px, 8.0 * px);
     if (use_sym_blur(c, L.oct[0].rows, L.oct[0].cols, batch))
-      launch_blur_base_sym(st, src, c->d_gpyr + L.oct[0].g_off[0], L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
+      launch_blur_base_sym(st, src, c->d_gpyr + L.oct[0].g_off[0], L.oct[0].pitch, L.g_img, L.rows, L.cols, batch,
+                           c->sym_xcd);
     else
       launch_blur_plane(st, c->w_base, c->d_coef + c->coef_base_off, src, c->d_gpyr + L.oct[0].g_off[0],
                         L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
@@ -414,7 +420,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       const bool fuse = c->fuse_dec && o + 1 < L.n_oct && blur_fuses_decimation(L, o + 1);
       StageScope s(c, sym ? ST_BLUR_SYM : ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
       if (sym)
-        launch_blur_octave_sym(st, L, o, c->d_gpyr, batch, fuse);
+        launch_blur_octave_sym(st, L, o, c->d_gpyr, batch, fuse, c->sym_xcd);
       else if (blur_octave_tiles(L, o, batch) < c->small_max)
         launch_blur_octave_small(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch, fuse);
       else
@@ -477,7 +483,7 @@ void enqueue_status(sift_ctx* c, bool check_cand, const int* img_off, int batch,
 int take_status(sift_ctx* c, bool sticky, int mask, bool kp_internal = false) {
   const int ct = c->h_stat[0], n = c->h_stat[1];
   int e = (sticky ? c->h_stat[3] : c->h_stat[2]) & mask;
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < 4; ++i)
     if (e & (1 << i)) HIP_TRY(c, hipMemsetAsync(c->d_err + i, 0, sizeof(int), c->stream));
   c->h_stat[2] &= ~e;
   c->h_stat[3] &= ~e;
@@ -487,6 +493,8 @@ int take_status(sift_ctx* c, bool sticky, int mask, bool kp_internal = false) {
     return fail(c, SIFT_E_WORKSPACE,
                 "candidate workspace overflow: capacity " + std::to_string(c->D.cand_cap) + " < " +
                     std::to_string(ct) + " extrema (sift_set_candidate_capacity, or a larger context)");
+  if (e & kErrStall)
+    return fail(c, SIFT_E_HIP, "an in-kernel pipeline wait expired (pyramid_pc.hip): the SIFT_FLAG_FAST planes are invalid");
   if (e & kErrAssert)
     return fail(c, SIFT_E_INVALID,
                 "keypoint octave/layer outside the pyramid (CV_Assert at src/sift.cpp:744)");
@@ -494,7 +502,7 @@ int take_status(sift_ctx* c, bool sticky, int mask, bool kp_internal = false) {
                                       " exceeds the output capacity (see d_img_offsets[batch])");
 }
 
-constexpr int kAllErr = kErrAssert | kErrWorkspace | kErrKpCapacity;
+constexpr int kAllErr = kErrAssert | kErrWorkspace | kErrKpCapacity | kErrStall;
 
 // ---- hipGraph cache --------------------------------------------------------
 template <typename T>
@@ -750,6 +758,10 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     c->fuse_dec = !(fd && atoi(fd) == 0);
     const char* pp = getenv("SIFT_HIP_POISON_PAD");
     c->poison_pad = pp && atoi(pp) != 0;
+    const char* pt = getenv("SIFT_HIP_PYR_TRI");
+    c->pyr_tri = pt && atoi(pt) != 0;
+    const char* sx = getenv("SIFT_HIP_SYM_XCD");
+    c->sym_xcd = sx && atoi(sx) != 0;
   }
   MathConsts mc;
   host_math_consts(&mc);

@@ -500,7 +500,23 @@ struct SymArgs {
   int rows, cols, strips, batch;
   int start[5];        // first wave of each slot; start[nslot] = grid size
   int chunk[4];        // output rows per wave, per slot
+  int count[4];        // waves of each slot (xcd: start[] spaced by count rounded up to 8)
+  int xcd;             // XCD-contiguous order (SIFT_HIP_SYM_XCD=1, A/B): blocks b, b + 8, ... take consecutive waves
 };
+
+// Wave index within slot `slot` of block `wid`; -1: a padding block.  With
+// A.xcd the blocks of one XCD (b, b + 8, ... under round-robin placement,
+// speed only) take a contiguous run of the slot's waves, so neighbouring
+// strips -- which read each other's w halo columns -- meet in one L2.
+__device__ __forceinline__ int sym_local(const SymArgs& A, int slot, int wid) {
+  int local = wid - A.start[slot];
+  if (A.xcd) {
+    const int n8 = A.start[slot + 1] - A.start[slot];
+    local = (local & 7) * (n8 >> 3) + (local >> 3);
+    if (local >= A.count[slot]) return -1;
+  }
+  return local;
+}
 
 // Wave-scope ordering of LDS accesses across lanes: no instruction, but the
 // compiler may not move loads or stores across it.
@@ -617,7 +633,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void bl
   asm volatile("; hold v160-v167" ::: "v160", "v167");
   const int wid = blockIdx.x;
   const int slot = wid >= A.start[3] ? 3 : wid >= A.start[2] ? 2 : wid >= A.start[1] ? 1 : 0;
-  const int local = wid - A.start[slot];
+  const int local = sym_local(A, slot, wid);
+  if (local < 0) return;
   switch (slot) {
     case 0: sym_walk<4>(A, 0, local, ring); break;
     case 1: sym_walk<3>(A, 1, local, ring); break;
@@ -629,7 +646,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void bl
 // The octave-0 base (createInitialImage's blur of the input, table 0).
 __global__ __launch_bounds__(64) void blur_sym_base_kernel(SymArgs A) {
   __shared__ float ring[SymSeg<kSymW0>::RING];
-  sym_walk<0>(A, 0, blockIdx.x, ring);
+  const int local = sym_local(A, 0, blockIdx.x);
+  if (local < 0) return;
+  sym_walk<0>(A, 0, local, ring);
 }
 
 bool sym_tables_match(const float* coefs) {
@@ -693,14 +712,16 @@ static void sym_plan(SymArgs& A, const int* w, int nslot, double cp) {
     ch = (A.rows + h - 1) / h;
     A.chunk[s] = h;
     A.start[s] = start;
-    start += A.strips * A.batch * ch;
+    A.count[s] = A.strips * A.batch * ch;
+    start += A.xcd ? (A.count[s] + 7) / 8 * 8 : A.count[s];
   }
   for (int s = nslot; s < 5; ++s) A.start[s] = start;
 }
 
 void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitch, long long dimg, int rows,
-                          int cols, int batch) {
+                          int cols, int batch, bool xcd) {
   SymArgs A{};
+  A.xcd = xcd;
   A.src = src.p;
   A.s_pitch = src.pitch;
   A.s_img = src.img_stride;
@@ -716,9 +737,11 @@ void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitc
   hipLaunchKernelGGL(blur_sym_base_kernel, dim3(A.start[1]), dim3(64), 0, st, A);
 }
 
-void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next) {
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next,
+                            bool xcd) {
   const Octave& O = L.oct[o];
   SymArgs A{};
+  A.xcd = xcd;
   const NextPlane nx = next_plane(L, o, gpyr, fuse_next);
   A.nxt = nx.p;
   A.n_pitch = nx.pitch;

@@ -227,8 +227,9 @@ long long blur_octave_tiles(const Layout& L, int o, int batch);
 // context's base + octave tables before these are used.
 bool sym_tables_match(const float* coefs);
 void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitch, long long dimg, int rows,
-                          int cols, int batch);
-void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next);
+                          int cols, int batch, bool xcd);
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next,
+                            bool xcd);
 void launch_decimate(hipStream_t st, const Layout& L, int o, float* gpyr, int batch);
 void launch_dog(hipStream_t st, const Layout& L, int o, const float* gpyr, float* dog, int batch);
 void launch_blur_1d(hipStream_t st, int w, const float* coef1d, Plane src, float* tmp, float* dst,
@@ -250,6 +251,17 @@ void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int n
 // fast_taps_host's for these sigmas; pyramid_tri_fits: every plane and the
 // input rows below the kernel's dropped-offset range.
 void launch_pyramid_tri(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
+// pyramid_pc.hip (default since round 5): the same planes, bit for bit, from a
+// producer wave and three consumer waves synchronised by LDS counters; err =
+// the context's sticky word err[3] (kErrStall).  SIFT_HIP_PYR_TRI=1 selects
+// pyramid_tri.hip.
+void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch, int* err);
+// Work items of one separable-pyramid launch (pyramid_tri.hip): n_full strip
+// columns walked whole, then the rest in `chunks` row chunks of `chunk` rows.
+struct TriPlan {
+  int n_full, chunk, chunks;
+};
+TriPlan tri_plan(int columns, int rows, int slots, int halo);
 bool pyramid_fuses_decimation(const Layout& L, int o);
 bool fast_taps_match(float sigma_base, const float* sig);
 bool pyramid_tri_fits(const Layout& L, long long src_row_stride);
@@ -285,6 +297,7 @@ void launch_emit(hipStream_t st, DetectBufs& D, int batch, sift_keypoint* kpts, 
 constexpr int kErrAssert = 1;      // keypoint octave/layer outside the pyramid (CV_Assert)
 constexpr int kErrWorkspace = 2;   // candidate workspace overflow
 constexpr int kErrKpCapacity = 4;  // keypoint total above the output capacity
+constexpr int kErrStall = 8;       // a bounded in-kernel wait expired (pyramid_pc.hip); err[3]
 void launch_status(hipStream_t st, const int* cand_total, int cand_cap, const int* img_off, int batch, int kp_cap,
                    int* err, int* stat);
 

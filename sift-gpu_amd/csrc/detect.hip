@@ -1688,13 +1688,15 @@ __global__ void status_kernel(const int* __restrict__ cand_total, int cand_cap, 
   if (threadIdx.x != 0) return;
   const int ct = cand_total ? *cand_total : 0;
   const int n = img_off ? img_off[batch] : 0;
-  const int fresh = (err[0] ? kErrAssert : 0) | (ct > cand_cap ? kErrWorkspace : 0) | (n > kp_cap ? kErrKpCapacity : 0);
+  const int fresh = (err[0] ? kErrAssert : 0) | (ct > cand_cap ? kErrWorkspace : 0) | (n > kp_cap ? kErrKpCapacity : 0) |
+                    (err[3] ? kErrStall : 0);
   if (fresh & kErrWorkspace) err[1] = 1;
   if (fresh & kErrKpCapacity) err[2] = 1;
   stat[0] = ct;
   stat[1] = n;
   stat[2] = fresh;
-  stat[3] = (err[0] ? kErrAssert : 0) | (err[1] ? kErrWorkspace : 0) | (err[2] ? kErrKpCapacity : 0);
+  stat[3] = (err[0] ? kErrAssert : 0) | (err[1] ? kErrWorkspace : 0) | (err[2] ? kErrKpCapacity : 0) |
+            (err[3] ? kErrStall : 0);
 }
 
 void launch_status(hipStream_t st, const int* cand_total, int cand_cap, const int* img_off, int batch, int kp_cap,

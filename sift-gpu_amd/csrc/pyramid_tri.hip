@@ -574,9 +574,6 @@ bool fast_taps_match(float sigma_base, const float* sig) {
 // cut every column into equal chunks (64 x 1080p octave 0: 5 rounds of 272 +
 // 60 rows = 1,660 rows per slot; the mixed plan: 1,080 + 60, then 270 + 60 =
 // 1,470).
-struct TriPlan {
-  int n_full, chunk, chunks;
-};
 TriPlan tri_plan(int columns, int rows, int slots, int halo) {
   static std::mutex mu;
   static std::map<std::array<int, 4>, TriPlan> cache;

@@ -230,13 +230,16 @@ def test_scatter_blur_pyramid_bitexact(siftgpu, oracle, monkeypatch, shape, b):
         assert_bits_equal(p, q, f"gpyr plane {i}")
 
 
-@pytest.mark.parametrize("mode", ["sym", "gather", "small"])
+@pytest.mark.parametrize("mode", ["sym", "sym_xcd", "gather", "small"])
 def test_blur_paths_1080p_and_8k_planes(siftgpu, oracle, monkeypatch, mode):
     """Every blur path at full size against the CPU path's plane digests: the
     scatter walk's multi-chunk plans (a 1080p or 8K image is split into
-    chunks per scale), the 2-D 8-pixel tiles, and the 2-output tiles of small
-    launches (blur_small_kernel) forced onto every octave."""
-    monkeypatch.setenv("SIFT_HIP_SYM_MIN", "0" if mode == "sym" else "1000000000")
+    chunks per scale), the same in XCD-contiguous wave order
+    (SIFT_HIP_SYM_XCD=1, padding blocks included), the 2-D 8-pixel tiles, and
+    the 2-output tiles of small launches (blur_small_kernel) forced onto every
+    octave."""
+    monkeypatch.setenv("SIFT_HIP_SYM_XCD", "1" if mode == "sym_xcd" else "0")
+    monkeypatch.setenv("SIFT_HIP_SYM_MIN", "0" if mode.startswith("sym") else "1000000000")
     monkeypatch.setenv("SIFT_HIP_SYM_ROWS_MIN", "0")
     monkeypatch.setenv("SIFT_HIP_SMALL_MAX", "1000000000" if mode == "small" else "0")
     for name, (R, C) in (("synth0_1080x1920", (1080, 1920)), ("synth0_4320x7680", (4320, 7680))):

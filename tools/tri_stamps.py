@@ -7,19 +7,18 @@
 Runs the SIFT_FLAG_FAST pyramid of configs[2] (64 x 1920x1080, device-resident
 synthetic images), reads the per-(octave, role, segment) s_memtime sums and
 prints, per octave and role, the average cycles per step in each segment and
-its share of the wave's lifetime.  Segments (stamp order within a step):
-  vmwait  s_waitcnt vmcnt(N) for the step's source rows (io roles; on gfx9 it
-          also waits for every older store)
-  barA    the step's first s_barrier (LDS drained by the stamp before it)
+its share of the wave's lifetime.  Segments (stamp order within a step; round-5 form of the shipped kernel):
+  vmwait  s_waitcnt vmcnt(N) for the step's own LDS-DMA source rows (io roles;
+          on gfx9 it also waits for every older store)
+  bar     the step's one s_barrier (LDS drained by the stamp before it)
   dma     issuing the next step's LDS-DMA source rows (io roles)
-  brow    octave 0: base row pass (io roles; idle role 0 goes straight on)
-  barB    octave 0: second barrier
-  bcol    octave 0: base column pass + plane-0 stores + LDS base rows
-  barC    octave 0: third barrier
-  row     row pass of the role's scales (LDS window reads, FMAs, h writes)
-  xpose   wave sync + column reads of the h rows
+  base    octave 0: base blur one step ahead -- row pass, wave sync, column
+          pass, LDS base rows, plane-0 transpose + stores (io roles)
+  row     row pass of the role's scales (LDS window reads, FMAs, h writes), 2 rounds
+  xpose   wave syncs + column reads of the h rows, 2 rounds
   col     column-pass FMAs (register scatter)
-  store   plane stores (buffer_store_dword)
+  stx     store transposes through the h rows (writes, sync, b128 reads), 2 rounds
+  store   plane store issue (dwordx4 / dwordx2), 2 rounds
   loop    loop overhead between steps
 Each stamp is s_memtime behind s_waitcnt lgkmcnt(0), so a segment's own LDS
 latency is charged to it and the instrumented kernel runs slower than the
@@ -37,7 +36,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "sift-gpu_amd"))
 import siftgpu  # noqa: E402
 
-SEGS = ["vmwait", "barA", "dma", "brow", "barB", "bcol", "barC", "row", "xpose", "col", "store", "loop"]
+SEGS = ["vmwait", "bar", "dma", "base", "row", "xpose", "col", "stx", "store", "loop"]
 K_TOTAL, K_STEPS, K_LIVE, K_WAVES, NSEG = 12, 13, 14, 15, 16
 ROLES = ["role0 w18", "role1 w12+io", "role2 w8,w4+io+dec"]
 
@@ -53,7 +52,7 @@ def pyramid_ms(lib_path, B, R, C, reps, want_stamps):
     de = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
     off = torch.empty((B + 1,), dtype=torch.int32, device="cuda")
     L = siftgpu.lib()
-    buf = (ctypes.c_ulonglong * (5 * 8192 * 3 * NSEG))()
+    buf = (ctypes.c_ulonglong * (5 * 16384 * 3 * NSEG))()
     dbg = getattr(L, "sift_dbg_tri_stamps", None) if want_stamps else None
     if dbg:
         dbg.restype = ctypes.c_int
@@ -80,7 +79,7 @@ def pyramid_ms(lib_path, B, R, C, reps, want_stamps):
         torch.cuda.synchronize()
         assert dbg(buf, 0) > 0
         import numpy as np
-        arr = np.frombuffer(buf, dtype=np.uint64).reshape(5, 8192, 3, NSEG).sum(axis=1)
+        arr = np.frombuffer(buf, dtype=np.uint64).reshape(5, 16384, 3, NSEG).sum(axis=1)
         stamps = [[[int(arr[o, r, k]) for k in range(NSEG)] for r in range(3)] for o in range(5)]
     ctx.close()
     return ms, stamps

@@ -1,0 +1,142 @@
+// ubench_pyrmem.hip -- the separable pyramid's memory stream alone (no
+// arithmetic, no synchronisation between waves) on MI355X, to separate the
+// memory structure's own rate from the kernel's compute (round 5).
+//
+// 64 images x 1080 x 1920; a 256-thread workgroup per 64-column strip walks
+// the rows 8 per step like pyramid_pc.hip: wave 0 loads the step's source rows
+// (columns [x0 - 24, x0 + 88)) into an LDS ring and stores plane 0; waves 1-3
+// store plane 4, plane 3, planes 2 + 1 + the decimated next plane 0 as
+// dwordx4 stores of 4 rows x 64 columns.  25 B per pixel (4 read, 21 written).
+// Modes (one JSON line each):
+//   0 stores only
+//   1 stores + source rows by LDS-DMA buffer_load_dword (16 per step, the kernel's form)
+//   2 stores + source rows by global_load_lds_dwordx4 (4 per step)
+//   3 stores + source rows by global_load_dwordx4 into VGPRs + ds_write_b128
+//   4 source rows only (LDS-DMA dword)
+//   5 stores with 4 waves storing per workgroup, no loads (the pure-store ceiling)
+//   hipcc -O3 --offload-arch=gfx950 tools/ubench_pyrmem.hip -o tools/ubench_pyrmem && ./tools/ubench_pyrmem
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+constexpr int B = 64, R = 1080, C = 1920, STRIPS = C / 64;
+constexpr long long PLANE = (long long)R * C;
+constexpr int ROWW = 112;  // source row segment (floats)
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc mk(const float* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, 0x00020000);
+}
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+template <int MODE>
+__global__ __launch_bounds__(256) void pyrmem_kernel(const float* __restrict__ src, float* __restrict__ planes,
+                                                      float* __restrict__ nxt) {
+  __shared__ __attribute__((aligned(16))) float ring[2][8][128];
+  const int item = blockIdx.x;
+  const int b = item / STRIPS, x0 = (item % STRIPS) * 64;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float* simg = src + b * PLANE;
+  const Rsrc rs = mk(simg, PLANE * 4);
+  float* img = planes + (long long)b * 5 * PLANE;
+  const int sr = lane >> 4, xg = x0 + 4 * (lane & 15);
+  float4 v = make_float4(lane, 1.f, 2.f, 3.f);
+  for (int s = 0; s < R / 8; ++s) {
+    const int Ys = 8 * s;
+    if (wv == 0 && MODE >= 1 && MODE <= 4) {
+      float* slot = &ring[s & 1][0][0];
+      if constexpr (MODE == 1 || MODE == 4) {
+        const int c0 = x0 - 24 + lane, c1 = c0 + 64;
+        const unsigned v0 = c0 >= 0 && c0 < C - 1 ? c0 * 4u : 0x7f000000u;
+        const unsigned v1 = c1 >= 0 && c1 < C - 1 ? c1 * 4u : 0x7f000000u;
+        for (int i = 0; i < 8; ++i) {
+          const unsigned so = (unsigned)((Ys + i) * C * 4);
+          const unsigned l0 = __builtin_amdgcn_readfirstlane(
+              (unsigned)(size_t)(const __attribute__((address_space(3))) float*)(slot + i * 128));
+          asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, %3 offen lds" ::"s"(l0), "v"(v0), "s"(rs),
+                       "s"(so) : "memory", "m0");
+          if (lane < ROWW - 64)
+            asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, %3 offen lds" ::"s"(l0 + 256), "v"(v1),
+                         "s"(rs), "s"(so) : "memory", "m0");
+        }
+      } else if constexpr (MODE == 2) {
+        // 8 rows x 28 chunks of 16 B = 224 chunks: 4 instructions, lane -> (row, chunk)
+        for (int t = 0; t < 4; ++t) {
+          const int ch = min(64 * t + lane, 8 * 28 - 1);
+          const int i = ch / 28, k = ch - i * 28;
+          const int c = max(x0 - 24 + 4 * k, 0);
+          __builtin_amdgcn_global_load_lds((const void*)(simg + (long long)(Ys + i) * C + c),
+                                           (__attribute__((address_space(3))) void*)(slot + 64 * 4 * t), 16, 0, 0);
+        }
+      } else if constexpr (MODE == 3) {
+        float4 r[4];
+        for (int t = 0; t < 4; ++t) {
+          const int ch = min(64 * t + lane, 8 * 28 - 1);
+          const int i = ch / 28, k = ch - i * 28;
+          const int c = max(x0 - 24 + 4 * k, 0);
+          r[t] = *reinterpret_cast<const float4*>(simg + (long long)(Ys + i) * C + c);
+        }
+        for (int t = 0; t < 4; ++t) *reinterpret_cast<float4*>(slot + 4 * (64 * t + lane)) = r[t];
+      }
+    }
+    if (MODE == 4) continue;
+    // stores: every storing wave writes its planes for rows [Ys, Ys + 8)
+    const int nstore = MODE == 5 ? 4 : 4;
+    if (wv < nstore) {
+      const int pa = wv == 0 ? 0 : wv == 1 ? 4 : wv == 2 ? 3 : 2;
+      for (int r4 = 0; r4 < 8; r4 += 4) {
+        const int y = Ys + r4 + sr;
+        const unsigned off = (unsigned)(y * C + xg) * 4u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), mk(img + pa * PLANE, PLANE * 4),
+                                               (int)off, 0, 0);
+        if (wv == 3) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), mk(img + 1 * PLANE, PLANE * 4),
+                                                 (int)off, 0, 0);
+          const bool dn = (y & 1) == 0;
+          const unsigned offn = dn ? (unsigned)((y >> 1) * (C / 2) + (xg >> 1)) * 4u : 0x7f000000u;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(v.x, v.z)),
+                                                mk(nxt + b * (PLANE / 4), PLANE), (int)offn, 0, 0);
+        }
+      }
+      v.x += 1.f;
+    }
+  }
+}
+
+int main() {
+  float *src, *planes, *nxt;
+  if (hipMalloc(&src, (size_t)B * PLANE * 4) != hipSuccess || hipMalloc(&planes, (size_t)B * 5 * PLANE * 4) != hipSuccess ||
+      hipMalloc(&nxt, (size_t)B * PLANE) != hipSuccess)
+    return 1;
+  (void)hipMemset(src, 0, (size_t)B * PLANE * 4);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  const char* names[6] = {"stores_only", "stores+dma_dword", "stores+dma_dwordx4", "stores+load_dwordx4+ds_write",
+                          "dma_dword_only", "stores_4waves"};
+  for (int mode = 0; mode < 6; ++mode) {
+    float best = 1e9f;
+    for (int rep = 0; rep < 5; ++rep) {
+      (void)hipEventRecord(e0);
+      const dim3 g(B * STRIPS), blk(256);
+      switch (mode) {
+        case 0: hipLaunchKernelGGL(pyrmem_kernel<0>, g, blk, 0, 0, src, planes, nxt); break;
+        case 1: hipLaunchKernelGGL(pyrmem_kernel<1>, g, blk, 0, 0, src, planes, nxt); break;
+        case 2: hipLaunchKernelGGL(pyrmem_kernel<2>, g, blk, 0, 0, src, planes, nxt); break;
+        case 3: hipLaunchKernelGGL(pyrmem_kernel<3>, g, blk, 0, 0, src, planes, nxt); break;
+        case 4: hipLaunchKernelGGL(pyrmem_kernel<4>, g, blk, 0, 0, src, planes, nxt); break;
+        default: hipLaunchKernelGGL(pyrmem_kernel<5>, g, blk, 0, 0, src, planes, nxt); break;
+      }
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (ms < best) best = ms;
+    }
+    const double px = (double)B * PLANE;
+    const double bytes = mode == 4 ? px * 4 * ROWW / 64 : mode == 0 || mode == 5 ? px * 21 : px * 25;
+    printf("{\"mode\": \"%s\", \"ms\": %.3f, \"TBs_moved\": %.3f, \"TBs_at_24B_per_px\": %.3f}\n", names[mode], best,
+           bytes / (best * 1e-3) / 1e12, px * 24 / (best * 1e-3) / 1e12);
+  }
+  return 0;
+}
