@@ -764,8 +764,8 @@ def exact_block(a, world, B, R, C, S, res, tr):
 
 
 def fast_kernel():
-    """The SIFT_FLAG_FAST pyramid kernel (sift-gpu_amd/csrc/pyramid_tri.hip)."""
-    return "pyr_tri_kernel", "pyramid_tri.hip"
+    """The SIFT_FLAG_FAST pyramid kernel (sift-gpu_amd/csrc/pyramid_pc.hip)."""
+    return "pyr_pc_kernel", "pyramid_pc.hip"
 
 
 def fast_block(a, world, B, R, C, fast_res, tr):

@@ -127,11 +127,10 @@ struct sift_ctx {
   long long gpyr_elems = 0, dog_elems = 0;
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
-  bool fast_ok = false;           // SIFT_FLAG_FAST: pyramid_tri.hip's compiled-in taps equal the host's
+  bool fast_ok = false;           // SIFT_FLAG_FAST: pyramid_pc.hip's compiled-in taps equal the host's
   bool fuse_dec = true;           // 2-D tile blurs write the next plane 0 (SIFT_HIP_FUSE_DEC=0: decimate_kernel)
   bool poison_pad = false;        // test switch SIFT_HIP_POISON_PAD=1: NaN into every plane's pitch padding
-  bool pyr_tri = false;
-  bool sym_xcd = false;           // scatter blur in XCD-contiguous wave order (SIFT_HIP_SYM_XCD=1, A/B)           // SIFT_FLAG_FAST on pyramid_tri.hip (SIFT_HIP_PYR_TRI=1) instead of pyramid_pc.hip
+  bool sym_xcd = false;           // scatter blur in XCD-contiguous wave order (SIFT_HIP_SYM_XCD=1, A/B)
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
   long long small_max = 2048;
@@ -256,14 +255,14 @@ int check_dims(sift_ctx* c, int rows, int cols, int n_oct, int batch) {
   return SIFT_OK;
 }
 
-// SIFT_FLAG_FAST preconditions: pyramid_tri.hip's literal taps equal the host
+// SIFT_FLAG_FAST preconditions: pyramid_pc.hip's literal taps equal the host
 // formula, and every plane and the input rows stay below the buffer offset
 // its dropped loads and stores use (without the size check a plane
 // of ~530 M pixels would read real pixels as padding and write inside itself).
 int check_fast(sift_ctx* c, const Layout& L, long long src_row_stride) {
   if (!(c->flags & SIFT_FLAG_FAST)) return SIFT_OK;
   if (!c->fast_ok) return fail(c, SIFT_E_INVALID, "SIFT_FLAG_FAST: compiled-in separable taps differ from the host's");
-  if (!pyramid_tri_fits(L, src_row_stride))
+  if (!pyramid_fast_fits(L, src_row_stride))
     return fail(c, SIFT_E_SIZE,
                 "SIFT_FLAG_FAST: the octave-0 plane or the input rows exceed the separable pyramid's "
                 "2,130,706,432-byte buffer-offset range");
@@ -370,7 +369,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
     for (int o = 0; o < L.n_oct; ++o) {
       const double px = plane_px(L, o) * batch;
       const double taps = 2.0 * (9 + 17 + 25 + 37) + (o == 0 ? 2.0 * 9 : 0.0);
-      // pyramid_tri.hip: octave o-1's launch wrote plane 0 of octave o when
+      // pyramid_pc.hip: octave o-1's launch wrote plane 0 of octave o when
       // it is an exact half; otherwise decimate first (plane 0
       // is one of the five plane writes, the decimation's read is not
       // algorithmic, so it is outside the pyramid stage's bytes)
@@ -379,10 +378,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
         launch_decimate(st, L, o, c->d_gpyr, batch);
       }
       StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-      if (c->pyr_tri)
-        launch_pyramid_tri(st, L, o, c->d_gpyr, src, batch);
-      else
-        launch_pyramid_pc(st, L, o, c->d_gpyr, src, batch, c->d_err + 3);
+      launch_pyramid_pc(st, L, o, c->d_gpyr, src, batch, c->d_err + 3);
     }
     if (c->poison_pad) enqueue_poison_pad(c, L, batch);
     if (with_dog)
@@ -750,7 +746,7 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     const char* sm = getenv("SIFT_HIP_SMALL_MAX");
     if (sm) c->small_max = atoll(sm);
   }
-  // SIFT_FLAG_FAST: pyramid_tri.hip carries its 1-D taps as literals; a
+  // SIFT_FLAG_FAST: pyramid_pc.hip carries its 1-D taps as literals; a
   // mismatch with the host formula makes the flag an error (enqueue-time check)
   c->fast_ok = fast_taps_match(sb, sig_f);
   {
@@ -758,8 +754,6 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     c->fuse_dec = !(fd && atoi(fd) == 0);
     const char* pp = getenv("SIFT_HIP_POISON_PAD");
     c->poison_pad = pp && atoi(pp) != 0;
-    const char* pt = getenv("SIFT_HIP_PYR_TRI");
-    c->pyr_tri = pt && atoi(pt) != 0;
     const char* sx = getenv("SIFT_HIP_SYM_XCD");
     c->sym_xcd = sx && atoi(sx) != 0;
   }

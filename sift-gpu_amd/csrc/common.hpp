@@ -39,7 +39,7 @@ constexpr double kCvPi = 3.1415926535897932384626433832795;
 // number of half lines, so every odd image of a batch was misaligned.)
 // Invariant: the pitch padding columns [cols, pitch) of every plane hold
 // unspecified values.  SIFT_FLAG_FAST's dwordx4 / dwordx2 plane stores
-// (pyramid_tri.hip) write whole 4-column groups past cols there, and no kernel
+// (pyramid_pc.hip) write whole 4-column groups past cols there, and no kernel
 // reads a column >= cols of a Gaussian or DoG plane (every reader bounds its
 // columns by cols, and the sub-module API copies planes out row by row with
 // cols columns); tests/test_gpu_fast.py::test_fast_ignores_pitch_padding
@@ -245,26 +245,23 @@ void perspective_transform(const double* H, const float* xy, int n, float* out);
 int knn_splits(int nq, int nt);
 void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int nt, int k, int splits,
                    float2* part_d, int2* part_i, int* idx, float* dist);
-// pyramid_tri.hip (SIFT_FLAG_FAST): octave o's five planes by the separable
+// pyramid_pc.hip (SIFT_FLAG_FAST): octave o's five planes by the separable
 // form, plus octave o+1's plane 0 when pyramid_fuses_decimation(L, o + 1)
-// (else decimate first).  fast_taps_match: the compiled-in 1-D taps equal
-// fast_taps_host's for these sigmas; pyramid_tri_fits: every plane and the
+// (else decimate first), from a producer wave and three consumer waves
+// synchronised by LDS counters; err = the context's sticky word err[3]
+// (kErrStall).  fast_taps_match: the compiled-in 1-D taps equal
+// fast_taps_host's for these sigmas; pyramid_fast_fits: every plane and the
 // input rows below the kernel's dropped-offset range.
-void launch_pyramid_tri(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch);
-// pyramid_pc.hip (default since round 5): the same planes, bit for bit, from a
-// producer wave and three consumer waves synchronised by LDS counters; err =
-// the context's sticky word err[3] (kErrStall).  SIFT_HIP_PYR_TRI=1 selects
-// pyramid_tri.hip.
 void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch, int* err);
-// Work items of one separable-pyramid launch (pyramid_tri.hip): n_full strip
-// columns walked whole, then the rest in `chunks` row chunks of `chunk` rows.
-struct TriPlan {
-  int n_full, chunk, chunks;
-};
-TriPlan tri_plan(int columns, int rows, int slots, int halo);
 bool pyramid_fuses_decimation(const Layout& L, int o);
 bool fast_taps_match(float sigma_base, const float* sig);
-bool pyramid_tri_fits(const Layout& L, long long src_row_stride);
+bool pyramid_fast_fits(const Layout& L, long long src_row_stride);
+// Work items of one separable-pyramid launch: n_full strip columns walked
+// whole, then the rest in `chunks` row chunks of `chunk` rows.
+struct FastPlan {
+  int n_full, chunk, chunks;
+};
+FastPlan fast_plan(int columns, int rows, int slots, int halo);
 
 // detect.hip
 struct DetectBufs {

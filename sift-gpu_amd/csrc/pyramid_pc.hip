@@ -5,8 +5,9 @@
 // The separable form of src/sift.cpp:229-263 (every scale blurred from its
 // octave base with the reference's sigma, width floor(3 sigma) (:97) and zero
 // padding outside [0, rows-1) x [0, cols-1) (:116)) in exactly the operation
-// order of pyramid_tri.hip and oracle/sift_oracle.c's so_fast_pyramid, so the
-// planes are the same bits (tests/test_gpu_fast.py).
+// order of oracle/sift_oracle.c's so_fast_pyramid, so the planes are its bits
+// (tests/test_gpu_fast.py) -- and those of round 3-4's pyramid_tri.hip, which
+// this file replaces (git history keeps it).
 //
 // Why (profiles/r5_tri_stamps.txt, r5_tri_ablation.txt): pyramid_tri.hip's
 // three roles met at one s_barrier per step; role 0 (w = 18) waited there 37 %
@@ -39,7 +40,13 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <array>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <queue>
 #include <utility>
+#include <vector>
 
 namespace sift {
 
@@ -59,7 +66,7 @@ constexpr int kPHb = 104;            // octave-0 base row-pass ring row: columns
 constexpr int kPHbRows = 16;
 constexpr int kPImg = 2;             // image ring slots (steps)
 constexpr int kPollMax = 1 << 20;    // bound of every wait (~70 M cycles at s_sleep 1)
-constexpr unsigned kPDropV = 0x7f000000u;  // one offset part past every plane (pyramid_tri_fits)
+constexpr unsigned kPDropV = 0x7f000000u;  // one offset part past every plane (pyramid_fast_fits)
 
 struct PcFlags {
   int pub;      // steps published by the producer (relative to the walk's first step)
@@ -594,6 +601,91 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void p
 
 }  // namespace
 
+bool pyramid_fuses_decimation(const Layout& L, int o) {
+  return o > 0 && L.oct[o - 1].rows == 2 * L.oct[o].rows && L.oct[o - 1].cols == 2 * L.oct[o].cols;
+}
+
+bool pyramid_fast_fits(const Layout& L, long long src_row_stride) {
+  // every plane and the input rows below the dropped-offset part (octave 0 is
+  // the largest plane), and the input's row offsets in 32 bits
+  const long long plane = (long long)L.oct[0].rows * L.oct[0].pitch * 4;
+  const long long srcb = (long long)L.oct[0].rows * src_row_stride * 4;
+  return plane < (long long)kPDropV && srcb < (long long)kPDropV;
+}
+
+bool fast_taps_match(float sigma_base, const float* sig) {
+  const float sg[5] = {sigma_base, sig[0], sig[1], sig[2], sig[3]};
+  const int ws[5] = {4, 4, 8, 12, 18};
+  const float* tabs[5] = {kFastT0, kFastT1, kFastT2, kFastT3, kFastT4};
+  for (int t = 0; t < 5; ++t) {
+    float g[64];
+    if (fast_taps_host(sg[t], nullptr) != 2 * ws[t] + 1) return false;
+    fast_taps_host(sg[t], g);
+    for (int a = 0; a <= ws[t]; ++a)
+      if (__builtin_memcmp(&tabs[t][a], &g[ws[t] + a], 4) != 0 || __builtin_memcmp(&g[ws[t] - a], &g[ws[t] + a], 4) != 0)
+        return false;
+  }
+  return true;
+}
+
+// Work items of one launch: every strip column walks its rows plus `halo`
+// rows it does not output (the lead above, the tail below, octave 0's base
+// prologue), so short chunks cost halo, and the grid runs in rounds of
+// `slots` resident workgroups, so a ragged last round idles the chip.  The
+// plan: n_full columns walked whole, dispatched first, then the other
+// columns in `chunks` chunks each.  Candidates (n_full a multiple of slots, or
+// every column; 1-32 chunks) are scored by list-scheduling the items in
+// dispatch order on `slots` identical slots (cost = rows walked); round 3
+// cut every column into equal chunks (64 x 1080p octave 0: 5 rounds of 272 +
+// 60 rows = 1,660 rows per slot; the mixed plan: 1,080 + 60, then 270 + 60 =
+// 1,470).
+FastPlan fast_plan(int columns, int rows, int slots, int halo) {
+  static std::mutex mu;
+  static std::map<std::array<int, 4>, FastPlan> cache;
+  const std::array<int, 4> key{columns, rows, slots, halo};
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  FastPlan best{columns, rows, 1};
+  long long best_cost = -1, best_items = 0;
+  std::vector<int> fulls;
+  for (long long f = 0; f < columns; f += slots) fulls.push_back((int)f);
+  fulls.push_back(columns);
+  for (int nf : fulls)
+    for (int c = 1; c <= (nf == columns ? 1 : 32); ++c) {
+      const int ch = nf == columns ? rows : ((rows + c - 1) / c + kPB - 1) / kPB * kPB;
+      const int cc = nf == columns ? 1 : (rows + ch - 1) / ch;
+      if (cc != c) continue;  // the same chunking as a smaller c
+      // list scheduling in dispatch order: each item to the earliest free slot
+      std::priority_queue<long long, std::vector<long long>, std::greater<long long>> q;
+      for (int i = 0; i < std::min<long long>(slots, (long long)nf + (long long)(columns - nf) * cc); ++i) q.push(0);
+      auto put = [&](long long len) {
+        const long long t = q.top();
+        q.pop();
+        q.push(t + len + halo);
+      };
+      for (int i = 0; i < nf; ++i) put(rows);
+      for (int k = 0; k < cc; ++k)
+        for (int i = nf; i < columns; ++i) put(std::min(ch, rows - k * ch));
+      long long cost = 0;
+      while (!q.empty()) {
+        cost = std::max(cost, q.top());
+        q.pop();
+      }
+      const long long items = nf + (long long)(columns - nf) * cc;
+      if (best_cost < 0 || cost < best_cost || (cost == best_cost && items < best_items)) {
+        best_cost = cost;
+        best_items = items;
+        best = FastPlan{nf, ch, cc};
+      }
+    }
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = best;
+  return best;
+}
+
 // Octave o of the pyramid, all five planes, and the next octave's plane 0 when
 // it is an exact half (pyramid_fuses_decimation).  src: octave 0's input
 // images (ignored for o > 0: the source is plane 0 of octave o).
@@ -628,7 +720,7 @@ void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plan
   A.columns = A.strips * batch;
   const int resident = resident_grid(o > 0 ? (const void*)pyr_pc_kernel<false> : (const void*)pyr_pc_kernel<true>,
                                      256, 0, 1024);
-  const TriPlan P = tri_plan(A.columns, O.rows, resident, kPLead + kPH + 2 + (o == 0 ? kPB : 0));
+  const FastPlan P = fast_plan(A.columns, O.rows, resident, kPLead + kPH + 2 + (o == 0 ? kPB : 0));
   A.n_full = P.n_full;
   A.chunk = P.chunk;
   A.chunks = P.chunks;

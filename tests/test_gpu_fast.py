@@ -1,5 +1,5 @@
 """GPU tests of SIFT_FLAG_FAST: the separable row/column Gaussian pyramid
-(sift-gpu_amd/csrc/pyramid_tri.hip) in front of the exact downstream kernels.
+(sift-gpu_amd/csrc/pyramid_pc.hip) in front of the exact downstream kernels.
 
 Fast mode is NOT bit-exact with the reference's 2-D float chain
 (src/sift.cpp:137-146): it applies K[a][b] = 8192 g(a) g(b) as a row pass and
@@ -40,9 +40,9 @@ def fctx(siftgpu):
 
 @pytest.mark.parametrize("shape,b", SHAPES + [((4320, 7680), 1)])
 def test_fast_pyramid_equals_its_oracle(siftgpu, oracle, shape, b):
-    """Every plane of pyr_tri_kernel == so_fast_pyramid, bit for bit (the
-    base blur one step ahead of the scales, chunk seams, strip edges, odd
-    shapes, a 4100-column strip count, the 8K image)."""
+    """Every plane of pyr_pc_kernel == so_fast_pyramid, bit for bit (the
+    producer wave's base blur, the consumers' register transposes, chunk
+    seams, strip edges, odd shapes, a 4100-column strip count, the 8K image)."""
     img = oracle.synth_image(b, *shape)
     ctx = siftgpu.Context(*shape, 1, device=0, flags=FAST)
     try:

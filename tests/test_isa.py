@@ -51,7 +51,8 @@ def test_orientation_checker_fails_without_the_barrier(tmp_path):
 
 
 def test_fast_pyramid_vmcnt_accounting():
-    """pyr_tri_kernel: no spills or scratch (vector-memory ops its hand-counted
-    vmcnt waits do not know about) and only the expected waits."""
-    out = _run("check_tri_isa.py")
+    """pyr_pc_kernel: no spills or scratch (vector-memory ops its hand-counted
+    vmcnt waits do not know about), only the producer's expected waits, one
+    s_barrier (the LDS counters' initialisation) and the register transposes."""
+    out = _run("check_pc_isa.py")
     assert out.count(" 0 violations") == 2, out

@@ -7,7 +7,7 @@
 #   fetch/write  --pmc FETCH_SIZE / WRITE_SIZE over bench.py (one step each)
 #   cal_f/cal_w  the same counters over tools/fetch_calib (known byte counts)
 #   sqA..sqC   SQ / GRBM / TCC counter groups over tools/stage_bench.py for the
-#              named kernels (exact path), sqF* the same for pyr_tri_kernel (SIFT_FLAG_FAST default)
+#              named kernels (exact path), sqF* the same for pyr_pc_kernel (SIFT_FLAG_FAST default)
 # usage: tools/profile.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r2}; shift
@@ -37,7 +37,7 @@ for grp in "$GA" "$GB" "$GC"; do
   i=$((i+1))
   run sq$i 300 --kernel-trace --pmc $grp -T --kernel-include-regex "$RE" -d $OUT/sq$i -o run --output-format csv -- \
     python3 tools/stage_bench.py --reps 1
-  run sqF$i 300 --kernel-trace --pmc $grp -T --kernel-include-regex "pyr_tri" -d $OUT/sqF$i -o run --output-format csv -- \
+  run sqF$i 300 --kernel-trace --pmc $grp -T --kernel-include-regex "pyr_pc" -d $OUT/sqF$i -o run --output-format csv -- \
     python3 tools/stage_bench.py --reps 1 --fast
 done
 run single 200 --kernel-trace --stats -T -d $OUT/single -o run --output-format csv -- \

@@ -33,7 +33,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STREAMING = re.compile(r"blur_octave_kernel|blur_plane_kernel|blur_sym_kernel|blur_sym_base_kernel|pyr_tri_kernel|dog_extrema_kernel|extrema_walk_kernel|decimate_kernel|"
+STREAMING = re.compile(r"blur_octave_kernel|blur_plane_kernel|blur_sym_kernel|blur_sym_base_kernel|pyr_pc_kernel|dog_extrema_kernel|extrema_walk_kernel|decimate_kernel|"
                        r"dog_kernel|blur1d|synth_kernel|grad_kernel|mask_count|mask_expand|bgr8_gray")
 
 
