@@ -71,7 +71,10 @@ constexpr unsigned kPDropV = 0x7f000000u;  // one offset part past every plane (
 struct PcFlags {
   int pub;      // steps published by the producer (relative to the walk's first step)
   int done[3];  // steps consumed by each consumer
+  int hpub;     // octaves > 0: steps whose w = 18 row pass the producer has written to h18
+  int hdone;    // octaves > 0: steps whose h18 rows consumer 0 has read
 };
+constexpr int kPH18 = 3;  // octaves > 0: h18 ring depth (steps)
 struct PcLds0 {  // octave 0: 32,272 B -> 5 workgroups per CU (96 VGPRs: 5 waves per SIMD)
   float base[kPD][kPB][kPPit];
   float img[kPImg][kPB][kPIW];
@@ -79,8 +82,9 @@ struct PcLds0 {  // octave 0: 32,272 B -> 5 workgroups per CU (96 VGPRs: 5 waves
   float tr0[kPB][kPW];   // producer's plane-0 store transpose
   PcFlags f;
 };
-struct PcLdsN {  // octave > 0
+struct PcLdsN {  // octave > 0: 22,552 B
   float base[kPD][kPB][kPPit];
+  float h18[kPH18][kPB][kPW];  // w = 18 row-pass output, lane = column 4i + R (pc_xpose4 layout)
   PcFlags f;
 };
 static_assert(sizeof(PcLds0) * 5 <= 163840, "five octave-0 workgroups per CU");
@@ -452,12 +456,30 @@ __device__ __forceinline__ void pc_producerN(const PcArgs& A, PcLdsN& L, int b, 
   issue(0);
   if (nsteps > 1) issue(1);
   for (int s = 0; s < nsteps; ++s) {
+    const int Ys = Ystart + kPB * s;
     // step s's rows landed: everything but step s + 1's loads (if issued)
     if (s + 1 < nsteps)
       PC_WAIT_VM(kPerStep);
     else
       PC_WAIT_VM(0);
     pc_publish(&L.f.pub, s + 1);
+    // The w = 18 row pass (consumer 0's, which would otherwise be the pole of
+    // every octave > 0 -- profiles/r5_pc_stamps.txt -- while this wave idles)
+    // into h18 slot s % kPH18, read by consumer 0 as lane = column 4i + R
+    if (Ys + kPB - 1 + kPH >= y0 && Ys - kPH < y1) {
+      pc_wait_ge(&L.f.hdone, s - kPH18 + 1, A.err);
+      const float* brow = &L.base[s % kPD][lane >> 4][4 * (lane & 15)];
+      float* hs = &L.h18[s % kPH18][0][0];
+#pragma unroll
+      for (int r4 = 0; r4 < kPB; r4 += 4) {
+        float h1[4], h2[4];
+        pc_rows<kPH, 0>(brow + r4 * kPPit, h1, h2);
+        pc_xpose4(h1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hs[(r4 + k) * kPW + lane] = h1[k];
+      }
+    }
+    pc_publish(&L.f.hpub, s + 1);
     if (s + 2 < nsteps) {
       pc_wait_done(L.f, s + 2 - kPD + 1, A.err);  // slot (s + 2) % kPD free
       issue(s + 2);
@@ -499,11 +521,18 @@ __device__ __forceinline__ void pc_consumer(const PcArgs& A, LdsT& L, int b, int
     // the step's source rows [Ys, Ys + 8) reach outputs [Ys - W1, Ys + 7 + W1] only
     const bool live = Ys + kPB - 1 + W1 >= y0 && Ys - W1 < y1;
     if (live) {
+      float c1[kPB], c2[kPB], o1[kPB], o2[kPB];
+      if constexpr (!OCT0 && C == 0) {
+        // octaves > 0: the producer ran this scale's row pass (pc_producerN)
+        pc_wait_ge(&L.f.hpub, s + 1, A.err);
+        const float* hs = &reinterpret_cast<PcLdsN&>(L).h18[s % kPH18][0][0];
+#pragma unroll
+        for (int j = 0; j < kPB; ++j) c1[j] = hs[j * kPW + lane];
+      } else {
       pc_wait_ge(&L.f.pub, s + 1, A.err);
       const float* brow = &L.base[s % kPD][lane >> 4][4 * (lane & 15)];
       // ---- row pass (lane = row R, 4 columns), two rounds of 4 rows, turned
       // into lane = column 4i + R by the register transpose ----
-      float c1[kPB], c2[kPB], o1[kPB], o2[kPB];
 #pragma unroll
       for (int r4 = 0; r4 < kPB; r4 += 4) {
         float h1[4], h2[4];
@@ -516,6 +545,7 @@ __device__ __forceinline__ void pc_consumer(const PcArgs& A, LdsT& L, int b, int
 #pragma unroll
           for (int k = 0; k < 4; ++k) c2[r4 + k] = h2[k];
         }
+      }
       }
       // ---- column pass (lane = column 4i + R), phase M of the role's slot cycle ----
       pc_col<W1, P1, M>(a1, c1, o1, std::make_integer_sequence<int, kPB>{});
@@ -541,14 +571,18 @@ __device__ __forceinline__ void pc_consumer(const PcArgs& A, LdsT& L, int b, int
         }
       }
     }
-    // every ring read of this step has been consumed: the slot may be refilled
-    pc_publish(&L.f.done[C], s + 1);
+    // every ring (h18) read of this step has been consumed: the slot may be refilled
+    if constexpr (!OCT0 && C == 0)
+      pc_publish(&L.f.hdone, s + 1);
+    else
+      pc_publish(&L.f.done[C], s + 1);
     ++s;
     return true;
   };
   while (pc_cycle(step, std::make_integer_sequence<int, NC>{})) {
   }
   pc_publish(&L.f.done[C], 1 << 30);  // never the producer's bottleneck again
+  if constexpr (!OCT0 && C == 0) pc_publish(&L.f.hdone, 1 << 30);
 }
 
 template <bool OCT0>
@@ -578,8 +612,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void p
   const int b = col / A.strips, x0 = (col - b * A.strips) * kPW;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (threadIdx.x == 0) {
-    L.f.pub = 0;
-    L.f.done[0] = L.f.done[1] = L.f.done[2] = 0;
+    L.f.pub = L.f.hpub = L.f.hdone = 0;
+    L.f.done[0] = OCT0 ? 0 : 1 << 30;  // octaves > 0: consumer 0 reads h18, not the ring
+    L.f.done[1] = L.f.done[2] = 0;
   }
   __syncthreads();  // the one workgroup barrier: counters initialised
   if (wv == 0) {

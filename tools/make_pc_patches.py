@@ -130,8 +130,10 @@ __device__ __forceinline__ void ps_flush(int oct, int wave, const PsAcc& ps, uns
   const unsigned long long ps_t0 = __builtin_amdgcn_s_memtime();
 ''')
     s = rep(s, '''      pc_wait_ge(&L.f.pub, s + 1, A.err);''', '''      pc_wait_ge(&L.f.pub, s + 1, A.err, ps);''')
-    s = rep(s, '''  pc_publish(&L.f.done[C], 1 << 30);  // never the producer's bottleneck again
-}''', '''  pc_publish(&L.f.done[C], 1 << 30);  // never the producer's bottleneck again
+    s = rep(s, '''        pc_wait_ge(&L.f.hpub, s + 1, A.err);''', '''        pc_wait_ge(&L.f.hpub, s + 1, A.err, ps);''')
+    s = rep(s, '''      pc_wait_ge(&L.f.hdone, s - kPH18 + 1, A.err);''', '''      pc_wait_ge(&L.f.hdone, s - kPH18 + 1, A.err, ps);''')
+    s = rep(s, '''  if constexpr (!OCT0 && C == 0) pc_publish(&L.f.hdone, 1 << 30);
+}''', '''  if constexpr (!OCT0 && C == 0) pc_publish(&L.f.hdone, 1 << 30);
   ps_flush(A.oct, C + 1, ps, ps_t0, nsteps);
 }''')
     s = rep(s, '''  A.err = err;
