@@ -776,7 +776,7 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   c->blk_cap = mask_blocks_per_image(L) * max_batch;
   if (dmalloc(&c->D.mask, (size_t)mask_words_per_image(L) * max_batch) != hipSuccess ||
       dmalloc(&c->D.blk_counts, c->blk_cap) != hipSuccess ||
-      dmalloc(&c->D.cand_total, 1) != hipSuccess ||
+      dmalloc(&c->D.cand_total, 1) != hipSuccess || dmalloc(&c->D.ori_next, 8) != hipSuccess ||
       dmalloc(&c->D.img_cand_off, max_batch + 1) != hipSuccess ||
       dmalloc(&c->D.kp_total, 1) != hipSuccess || dmalloc(&c->d_img_off, max_batch + 1) != hipSuccess ||
       alloc_candidates(c, (int)cap) != SIFT_OK)
@@ -799,8 +799,8 @@ int sift_ctx_destroy(sift_ctx* c) {
   if (c->h_stat) (void)hipHostFree(c->h_stat);
   void* bufs[] = {c->d_stat, c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
-                  c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles, c->d_img_off,
-                  c->d_kpts, c->d_desc, c->d_err, c->d_match};
+                  c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles, c->D.ori_next,
+                  c->d_img_off, c->d_kpts, c->d_desc, c->d_err, c->d_match};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);

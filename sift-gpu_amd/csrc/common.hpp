@@ -277,6 +277,7 @@ struct DetectBufs {
   int* npeaks;          // orientation peaks per candidate, [cand_cap]
   int* scan_tmp;        // exclusive scan of blk_counts, [blk_cap+1]
   int* scan_tiles;      // per-tile sums of the multi-block scan, [scan_tiles_for(max(blk_cap, cand_cap))]
+  int* ori_next;        // [8] per-XCD candidate counters of the one-image orientation pass (refine_kernel zeroes them)
 };
 int scan_tiles_for(long long cap);
 long long mask_words_per_image(const Layout& L);

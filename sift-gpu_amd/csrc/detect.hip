@@ -836,6 +836,7 @@ struct RefArgs {
   int cand_cap;
   CandOut* couts;
   int* npeaks;
+  int* ori_next;  // [8] orient_bin_kernel<true>'s per-XCD candidate counters
 };
 
 // adjustLocalExtrema (src/sift.cpp:287-388) for one candidate.
@@ -992,6 +993,9 @@ __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const flo
 // Refinement: one lane per candidate.  Writes the refined keypoint fields and
 // the orientation pass's inputs (refined r, c, layer; npeaks = 1 if kept).
 __global__ __launch_bounds__(256) void refine_kernel(RefArgs A) {
+  // the next launch on this stream is the orientation pass: its work counters
+  // start at 0 on every path (graph replay, direct launches, sub-module calls)
+  if (blockIdx.x == 0 && threadIdx.x < 8) A.ori_next[threadIdx.x] = 0;
   int n = *A.cand_total;
   if (n > A.cand_cap) n = A.cand_cap;
   for (int ci = blockIdx.x * 256 + threadIdx.x; ci < n; ci += gridDim.x * 256) {
@@ -1226,8 +1230,14 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
 // exactly the reference's adds in the reference's order.  Invalid samples
 // (outside the image interior, src/sift.cpp:405,410) join no bin; the masked
 // reads past a bin's count add +0.0 to a sum that is >= +0 (exact no-op).
+// DYN (speed only): each wave draws its next candidate of the XCD's range from
+// a per-XCD counter (A.ori_next, zeroed by refine_kernel, the launch before
+// this one on every path) instead of the fixed interleave ci += nw; the draw
+// for the next candidate is issued at the top of the body, so a rejected
+// candidate's `continue` still moves on, and every draw strictly increases.
 constexpr int kOBW = 4;  // waves per workgroup
 
+template <bool DYN>
 __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   __shared__ float vals[kOBW][64][kOriBins];  // [wave][rank][bin]: owner reads are conflict free
   __shared__ int cnt[kOBW][64];
@@ -1244,8 +1254,12 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   const int nw = (int)(gridDim.x >> 3) * kOBW;
   const int per = (n + 7) / 8;
   const int xcd = blockIdx.x & 7, wid = (int)(blockIdx.x >> 3) * kOBW + w;
-  const int cend = min(n, (xcd + 1) * per);
-  for (int ci = xcd * per + wid; ci < cend; ci += nw) {
+  const int c0 = xcd * per, cend = min(n, c0 + per);
+  int nxt = 0;
+  if (DYN && lane == 0) nxt = atomicAdd(&A.ori_next[xcd], 1);
+  for (int ci = c0 + (DYN ? __builtin_amdgcn_readfirstlane(nxt) : wid); ci < cend;
+       ci = DYN ? c0 + __builtin_amdgcn_readfirstlane(nxt) : ci + nw) {
+    if (DYN && lane == 0) nxt = atomicAdd(&A.ori_next[xcd], 1);
     const CandOut& co = A.couts[ci];
     if (co.npeaks == 0) {  // refinement rejected it
       if (lane == 0) A.npeaks[ci] = 0;
@@ -1620,6 +1634,7 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.cand_cap = D.cand_cap;
   A.couts = D.couts;
   A.npeaks = D.npeaks;
+  A.ori_next = D.ori_next;
   hipLaunchKernelGGL(refine_kernel, dim3(resident_grid((const void*)refine_kernel, 256, 0, 2048)), dim3(256), 0, st, A);
   // batches: two candidates per lane group (orient_slots_kernel<2>); one
   // image: one wave per candidate with bucketed bins (orient_bin_kernel,
@@ -1633,9 +1648,18 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
     return v >= 1 && v <= 5 ? v : 0;
   }();
   const int slots = slots_env ? slots_env : batch == 1 ? 5 : 2;
-  if (slots == 5)
-    hipLaunchKernelGGL(orient_bin_kernel, dim3(resident_grid((const void*)orient_bin_kernel, 64 * kOBW, 0, 2048)),
-                       dim3(64 * kOBW), 0, st, A);
+  static const bool dyn = [] {
+    const char* e = getenv("SIFT_HIP_ORIENT_DYN");  // A/B: per-XCD work counters in orient_bin_kernel
+    return e && atoi(e) != 0;
+  }();
+  if (slots == 5 && dyn)
+    hipLaunchKernelGGL(orient_bin_kernel<true>,
+                       dim3(resident_grid((const void*)orient_bin_kernel<true>, 64 * kOBW, 0, 2048)), dim3(64 * kOBW),
+                       0, st, A);
+  else if (slots == 5)
+    hipLaunchKernelGGL(orient_bin_kernel<false>,
+                       dim3(resident_grid((const void*)orient_bin_kernel<false>, 64 * kOBW, 0, 2048)), dim3(64 * kOBW),
+                       0, st, A);
   else if (slots == 1)
     hipLaunchKernelGGL(orient_kernel, dim3(resident_grid((const void*)orient_kernel, 64, 0, 8192)), dim3(64), 0, st,
                        A);

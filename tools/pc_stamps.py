@@ -5,7 +5,7 @@
   python tools/pc_stamps.py [--lib sift-gpu_amd/lib/libsift_hip_pcstamps.so] [--reps 5]
 
 Runs the SIFT_FLAG_FAST pyramid of configs[2] (64 x 1920x1080, device-resident
-synthetic images) and prints, per octave and wave (producer, w18, w12,
+synthetic images; --shape 1x4320x7680 for configs[4]) and prints, per octave and wave (producer, w18, w12,
 w8+w4), the average cycles per wave and per step and the share of the wave's
 lifetime spent in its LDS-counter waits (producer: for the slowest consumer
 to free a ring slot; consumers: for the producer to publish a step), with the
@@ -33,14 +33,15 @@ def main():
     p.add_argument("--lib", default=os.path.join(ROOT, "sift-gpu_amd", "lib", "libsift_hip_pcstamps.so"))
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--json", default="")
+    p.add_argument("--shape", default="64x1080x1920", help="BxROWSxCOLS (configs[4]: 1x4320x7680)")
     a = p.parse_args()
     siftgpu.LIB_PATH = a.lib
     siftgpu._lib = None
-    B, R, C = 64, 1080, 1920
+    B, R, C = (int(v) for v in a.shape.split("x"))
     ctx = siftgpu.Context(R, C, B, flags=siftgpu.SIFT_FLAG_PROFILE | siftgpu.SIFT_FLAG_FAST)
     imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
     ctx.synth_images(imgs.data_ptr(), B, R, C, C, R * C, 0)
-    cap = B * 40000
+    cap = max(B * 40000, 1 << 20)
     kp = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
     de = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
     off = torch.empty((B + 1,), dtype=torch.int32, device="cuda")
