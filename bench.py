@@ -876,6 +876,20 @@ def launch_ranks(a, argv=None) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def rehearsal():
+    """SIFT_BENCH_SHARE_GPU=1 (rehearsal only, never a reported run): N ranks
+    may share the visible devices (rank r on device r % count) and talk over
+    SIFT_BENCH_DIST_BACKEND (gloo: the gather stages through host memory), so
+    the N > 1 orchestration -- launcher, barriers, max-over-ranks timing, the
+    keypoint gather and rank 0's line -- runs on a one-GPU box, where RCCL
+    refuses two ranks on one device."""
+    return os.environ.get("SIFT_BENCH_SHARE_GPU", "0") == "1"
+
+
+def dist_backend():
+    return os.environ.get("SIFT_BENCH_DIST_BACKEND", "nccl") if rehearsal() else "nccl"
+
+
 def check_world(a):
     """The rank count the launcher gave us must be the one --gpus asks for,
     and the node must have that many devices (device_count does not
@@ -883,7 +897,7 @@ def check_world(a):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" in os.environ and world != a.gpus:
         return f"WORLD_SIZE={world} but --gpus {a.gpus}: launch one rank per requested GPU"
-    if a.gpus > 1:
+    if a.gpus > 1 and not rehearsal():
         n = torch.cuda.device_count()
         if a.gpus > n:
             return f"--gpus {a.gpus} but only {n} HIP device(s) visible"
@@ -896,7 +910,7 @@ def main():
         sys.exit("bench.py: --gpus must be >= 1")
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         n = torch.cuda.device_count()
-        if a.gpus > n:
+        if a.gpus > n and not rehearsal():
             sys.exit(f"bench.py: --gpus {a.gpus} but only {n} HIP device(s) visible")
         sys.exit(launch_ranks(a))
     GPU_ERROR_LEGS.clear()
@@ -913,8 +927,12 @@ def main():
         # child processes
         cpu = cpu_legs(a, errors)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = local % torch.cuda.device_count() if rehearsal() else local
+        torch.cuda.set_device(dev)
+        if dist_backend() == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(dist_backend())
     else:
         torch.cuda.set_device(0)
     env = Env(a, world, rank)
@@ -938,6 +956,9 @@ def main():
         out = assemble(a, world, (env.B, env.R, env.C, env.S), res, cpu, errors)
         out["distributed"] = {"world_size": world, "backend": dist.get_backend() if world > 1 else None,
                               "launcher": "torch.distributed.run" if "WORLD_SIZE" in os.environ else "none"}
+        if rehearsal():
+            out["distributed"]["rehearsal"] = ("SIFT_BENCH_SHARE_GPU=1: ranks share devices; not a "
+                                               "multi-GPU measurement")
         if a.profile_json and res.get("exact") is not None:
             with open(a.profile_json, "w") as f:
                 json.dump(res["exact"]["prof"][1], f, indent=1)

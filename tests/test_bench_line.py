@@ -2,6 +2,7 @@
 (a late-leg failure cost the driver's only bench record).  CPU
 test: the device legs are replaced by canned results, one leg raises."""
 import json
+import subprocess
 import sys
 import types
 
@@ -129,6 +130,29 @@ def test_gpus_more_than_devices_fails(bench, monkeypatch):
     with pytest.raises(SystemExit) as ex:
         bench.main()
     assert ex.value.code not in (0, None) and "only 1" in str(ex.value.code)
+
+
+def test_shared_gpu_rehearsal_launches_past_the_device_count(bench, monkeypatch):
+    """SIFT_BENCH_SHARE_GPU=1: --gpus 2 on a one-device box still launches two
+    ranks (the rehearsal of the N > 1 path); without it the same call fails."""
+    import torch
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("SIFT_BENCH_SHARE_GPU", "1")
+    monkeypatch.setenv("SIFT_BENCH_DIST_BACKEND", "gloo")
+    seen = {}
+
+    def fake_run(cmd, env=None, **k):
+        seen["cmd"] = cmd
+        return subprocess.CompletedProcess(cmd, 0)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 0 and "--nproc-per-node=2" in seen["cmd"]
+    assert bench.dist_backend() == "gloo" and bench.check_world(bench.parse()) is None
+    monkeypatch.setenv("SIFT_BENCH_SHARE_GPU", "0")
+    assert bench.dist_backend() == "nccl"
 
 
 def test_line_carries_world_and_launcher(bench, monkeypatch, capsys):
