@@ -214,7 +214,8 @@ int main() {
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (ms < best) best = ms;
     }
-    const double px = (double)B * PLANE;
+    // modes 11 and 16 cover C / 256 * 256 = 1,792 of the 1,920 columns: count the bytes they move
+    const double px = (double)B * PLANE * (mode == 11 || mode == 16 ? (C / 256 * 256) / (double)C : 1.0);
     const double bytes = mode == 4 ? px * 4 * ROWW / 64 : mode == 0 || mode == 5 ? px * 21 : mode == 9 ? px * 8
                          : mode == 13 ? px * 8 : mode == 14 ? px * 21 : px * 25;
     printf("{\"mode\": \"%s\", \"ms\": %.3f, \"TBs_moved\": %.3f, \"TBs_at_24B_per_px\": %.3f}\n", names[mode], best,
