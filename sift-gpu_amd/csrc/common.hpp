@@ -263,6 +263,15 @@ struct FastPlan {
 };
 FastPlan fast_plan(int columns, int rows, int slots, int halo);
 
+// One image small enough that the per-keypoint kernels are latency-bound (a
+// 1080p image: ~13 K candidates, a few waves per SIMD) runs their one-image
+// variants (orient_bin_kernel, the descriptor budgeted for 2 waves per SIMD);
+// a batch, or one image above kOneImagePx (an 8K image: 214 K keypoints),
+// fills the chip with the batch variants.  SIFT_HIP_ONE_IMAGE_PX overrides the
+// limit (A/B runs).
+constexpr long long kOneImagePx = 4ll << 20;
+bool one_image_variants(const Layout& L, int batch);
+
 // detect.hip
 struct DetectBufs {
   unsigned* mask;       // candidate bitmask, mask_words_per_image * batch

@@ -654,9 +654,10 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
     const char* e = getenv("SIFT_HIP_DESC_PACKED");  // A/B switch between the two record forms
     return !e || atoi(e) != 0;
   }();
-  // detected keypoints gather two batches ahead (PF = 2): one image per call
-  // is budgeted for 2 waves per SIMD (few waves, latency-bound chains),
-  // batches for kDescWpe; SIFT_HIP_DESC_DEEP=0 selects the one-ahead form
+  // detected keypoints gather two batches ahead (PF = 2): one image of up to
+  // kOneImagePx (one_image_variants) is budgeted for 2 waves per SIMD (few
+  // waves, latency-bound chains), batches and larger images for kDescWpe;
+  // SIFT_HIP_DESC_DEEP=0 selects the one-ahead form
   static const bool deep = [] {
     const char* e = getenv("SIFT_HIP_DESC_DEEP");
     return !e || atoi(e) != 0;
@@ -664,7 +665,7 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
 #define SIFT_DESC_LAUNCH(...)                                                                                       \
   hipLaunchKernelGGL((descriptor_kernel<__VA_ARGS__>),                                                              \
                      dim3(resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192)), dim3(64), 0, st, A)
-  if (packed && detected && deep && batch == 1)
+  if (packed && detected && deep && one_image_variants(L, batch))
     SIFT_DESC_LAUNCH(true, true, 2, 2);
   else if (packed && detected && deep)
     SIFT_DESC_LAUNCH(true, true, 2, kDescWpe);

@@ -1620,6 +1620,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2
   }
 }
 
+bool one_image_variants(const Layout& L, int batch) {
+  static const long long lim = [] {
+    const char* e = getenv("SIFT_HIP_ONE_IMAGE_PX");
+    return e ? atoll(e) : kOneImagePx;
+  }();
+  return batch == 1 && (long long)L.rows * L.cols <= lim;
+}
+
 void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, const float2* grad,
                           const float* dog, const MathConsts* mc, DetectBufs& D, int batch) {
   RefArgs A;
@@ -1647,7 +1655,7 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
     const int v = e ? atoi(e) : 0;
     return v >= 1 && v <= 5 ? v : 0;
   }();
-  const int slots = slots_env ? slots_env : batch == 1 ? 5 : 2;
+  const int slots = slots_env ? slots_env : one_image_variants(L, batch) ? 5 : 2;
   static const bool dyn = [] {
     const char* e = getenv("SIFT_HIP_ORIENT_DYN");  // A/B: per-XCD work counters in orient_bin_kernel
     return e && atoi(e) != 0;
