@@ -409,7 +409,7 @@ print(len(kps), sha(kps), sha(desc))
                                  {"SIFT_HIP_ORIENT_SLOTS": "4"}, {"SIFT_HIP_ORIENT_SLOTS": "5"},
                                  {"SIFT_HIP_DESC_PACKED": "0"},
                                  {"SIFT_HIP_FUSE_DEC": "0"}, {"SIFT_HIP_DESC_DEEP": "0"},
-                                 {"SIFT_HIP_ORIENT_DYN": "1"}])
+                                 {"SIFT_HIP_ORIENT_DYN": "1"}, {"SIFT_HIP_ONE_IMAGE_PX": "0"}])
 def test_kernel_variants_match_golden(env):
     """The A/B kernel variants the library keeps behind environment switches
     (read once per process, so each runs in a child process) give the same
