@@ -22,11 +22,14 @@
 //        steps in LDS -- octave 0: LDS-DMA of image rows, the base blur
 //        (createInitialImage, w = 4) row and column passes over the strip's
 //        100 base columns, plane 0 stored; octaves > 0: LDS-DMA of plane-0
-//        rows straight into the ring, two steps ahead;
+//        rows straight into the ring, two steps ahead, and the w = 18 scale's
+//        row pass into the h18 ring (hpub / hdone counters) -- above octave 0
+//        that wave would otherwise idle while the w = 18 consumer is the pole;
 //      waves 1-3 (consumers): plane 4 (w = 18), plane 3 (w = 12), planes 2
 //        and 1 (w = 8, 4, pair sums shared) + the next octave's decimated
-//        plane 0: row pass from the ring, column pass scattered into register
-//        accumulators, dwordx4 plane stores.
+//        plane 0: row pass from the ring (w = 18 above octave 0: from h18),
+//        column pass scattered into register accumulators, dwordx4 plane
+//        stores.
 //  * LDS counters: the producer publishes `pub` = steps whose base rows are
 //    in the ring; consumer c publishes done[c] = steps it has read.  A
 //    consumer waits only for pub, the producer only for the slowest consumer
