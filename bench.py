@@ -109,22 +109,29 @@ ORACLE_NOTE = ("oracle/sift_oracle.c: SIFT_NCL restated in C, gcc -O3 -ffp-contr
                "faster than the reference's own loop (conservative for speed-up claims)")
 
 
-def cpu_baseline(rows, cols, threads=1):
-    """One image, `threads` OpenMP threads (the reference's own split: the
-    descriptor loop, src/sift.cpp:738; the rest of the path is serial there)."""
+def cpu_baseline(rows, cols, threads=1, min_seconds=0.0, max_images=8):
+    """`threads` OpenMP threads (the reference's own split: the descriptor
+    loop, src/sift.cpp:738; the rest of the path is serial there) over
+    synthetic images of seeds 0, 1, ... until at least `min_seconds` of CPU
+    work (one image at least, `max_images` at most): the bounded sample the
+    rate is measured on."""
     O = _oracle()
     O.set_threads(threads)
-    img = O.synth_image(0, rows, cols)
-    t0 = time.perf_counter()
-    kps, _ = O.sift(img, 5)
-    dt = time.perf_counter() - t0
+    dt, nkp, n = 0.0, 0, 0
+    while n < max(1, max_images) and (n == 0 or dt < min_seconds):
+        img = O.synth_image(n, rows, cols)
+        t0 = time.perf_counter()
+        kps, _ = O.sift(img, 5)
+        dt += time.perf_counter() - t0
+        nkp += len(kps)
+        n += 1
     O.set_threads(1)
-    mpix = rows * cols / 1e6
+    mpix = n * rows * cols / 1e6
     return {"value": round(mpix / dt, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "keypoints_per_s": round(len(kps) / dt, 1), "seconds": round(dt, 3),
-            "sample": f"1 synthetic {cols}x{rows} image (seed 0), {threads} thread(s)"
+            "keypoints_per_s": round(nkp / dt, 1), "seconds": round(dt, 3),
+            "sample": f"{n} synthetic {cols}x{rows} image(s) (seeds 0..{n - 1}), {threads} thread(s)"
                       f"{' (OpenMP over descriptors, as the reference)' if threads > 1 else ''}, "
-                      f"{len(kps)} keypoints",
+                      f"{nkp} keypoints",
             "note": ORACLE_NOTE}
 
 
@@ -477,7 +484,8 @@ def cpu_legs(a, errors):
     """1 thread, OpenMP over descriptors, image-parallel."""
     nthr = min(16, int(os.environ.get("OMP_NUM_THREADS", "16")))
     cpu = {}
-    one = guarded(errors, "cpu_baseline", cpu_baseline, a.rows, a.cols)
+    # the 1-thread baseline: about 10 s of CPU work (3 images at ~3.2 s each)
+    one = guarded(errors, "cpu_baseline", cpu_baseline, a.rows, a.cols, 1, 9.0)
     if one is not None:
         cpu["cpu_baseline"] = one
     omp = guarded(errors, "cpu_baseline_omp", cpu_baseline, a.rows, a.cols, nthr)

@@ -36,7 +36,7 @@ def bench(monkeypatch):
     monkeypatch.setattr(B, "Env", FakeEnv)
     monkeypatch.setattr(B, "run_exact", lambda env: {"exact": (0.1, {}, 800000.0), "prof": (0.12, _stats(), 0.0),
                                                      "verified": [0, 31, 63], "failed": [], "gather": None})
-    monkeypatch.setattr(B, "cpu_baseline", lambda r, c, threads=1: {"value": 0.6, "unit": "Mpix/s", "cores": threads,
+    monkeypatch.setattr(B, "cpu_baseline", lambda r, c, threads=1, min_seconds=0.0: {"value": 0.6, "unit": "Mpix/s", "cores": threads,
                                                                     "kind": "port", "keypoints_per_s": 4000.0,
                                                                     "sample": "canned"})
     monkeypatch.setattr(B, "cpu_baseline_parallel", lambda r, c, w: None)
