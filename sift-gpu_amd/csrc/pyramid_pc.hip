@@ -719,6 +719,17 @@ FastPlan fast_plan(int columns, int rows, int slots, int halo) {
         best = FastPlan{nf, ch, cc};
       }
     }
+  // A chunked plan that fits one round starts every workgroup at once, and
+  // they then run their phases in lockstep (all DMA, then all arithmetic):
+  // one 8K image's octave 0 (1,200 items on 1,280 slots) ran 5 % faster with
+  // twice the chunks (0.397-0.401 vs 0.417-0.422 ms of pyramid,
+  // profiles/r5_pc_chunks_ab.txt), while three times was slower and the
+  // many-round 64 x 1080p plans do not change.  So such a plan takes twice
+  // the chunks when they stay at least twice the halo tall.
+  if (best.n_full < columns && (long long)(columns - best.n_full) * best.chunks + best.n_full <= slots) {
+    const int ch2 = ((rows + 2 * best.chunks - 1) / (2 * best.chunks) + kPB - 1) / kPB * kPB;
+    if (ch2 >= 2 * halo) best = FastPlan{best.n_full, ch2, (rows + ch2 - 1) / ch2};
+  }
   std::lock_guard<std::mutex> lk(mu);
   cache[key] = best;
   return best;
