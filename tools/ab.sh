@@ -8,6 +8,7 @@
 #            exact   tools/stage_bench.py: every exact-path stage time
 #            bench   bench.py's exact headline leg (2 streams, graph replay, --steps 10)
 #            single  bench.py's configs[1] one-image leg
+#            8k      bench.py's configs[4] leg (one 8K image: exact latency + fast-pyramid roofline)
 #   variant  <name>            lib/libsift_hip_<name>.so (tools/build_var.sh, tools/build_patch.sh);
 #                              "cur" = the current lib/libsift_hip.so
 #            VAR=val[,VAR=val] the current build with those environment settings
@@ -74,6 +75,15 @@ print(sys.argv[2], d['value'], d['ms_per_step'], 'serial', d['serial_leg']['ms_p
 import json, sys
 s = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]).get('single_image') or {}
 print(sys.argv[2], s.get('latency_ms'), s.get('device_no_graph_ms'), 'verified', s.get('output_verified'))" $f.json "$v" ;;
+      8k)
+        env $ENVS timeout -k 10 200 python3 bench.py --only 8k --steps 5 --warmup 2 $ARGS > $f.json 2> $f.err \
+          || { echo "8k $v failed"; tail -5 $f.err; exit 1; }
+        python3 -c "
+import json, sys
+e = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['image_8k']
+r = e['roofline']
+print(sys.argv[2], 'latency_ms', e['latency_ms'], 'blur_ms', r['exact_blur_octave']['ms_per_image'], 'fast_pyr_ms',
+      r['fast_pyramid']['ms_per_image'], 'frac', r['fast_pyramid']['frac'], 'verified', e['output_verified'])" $f.json "$v" ;;
       *) echo "unknown leg $LEG"; exit 2 ;;
     esac
   done
