@@ -130,7 +130,7 @@ struct sift_ctx {
   bool fast_ok = false;           // SIFT_FLAG_FAST: pyramid_pc.hip's compiled-in taps equal the host's
   bool fuse_dec = true;           // 2-D tile blurs write the next plane 0 (SIFT_HIP_FUSE_DEC=0: decimate_kernel)
   bool poison_pad = false;        // test switch SIFT_HIP_POISON_PAD=1: NaN into every plane's pitch padding
-  bool sym_xcd = false;           // scatter blur in XCD-contiguous wave order (SIFT_HIP_SYM_XCD=1, A/B)
+  bool sym_xcd = true;            // scatter blur in XCD-contiguous wave order (SIFT_HIP_SYM_XCD=0: launch order, A/B)
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
   long long small_max = 2048;
@@ -755,7 +755,9 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
     const char* pp = getenv("SIFT_HIP_POISON_PAD");
     c->poison_pad = pp && atoi(pp) != 0;
     const char* sx = getenv("SIFT_HIP_SYM_XCD");
-    c->sym_xcd = sx && atoi(sx) != 0;
+    // XCD-contiguous order by default (round 5): -36 % blur read traffic,
+    // headline equal or +0.1 % (profiles/r5_blur_xcd_ab.txt)
+    c->sym_xcd = !(sx && atoi(sx) == 0);
   }
   MathConsts mc;
   host_math_consts(&mc);

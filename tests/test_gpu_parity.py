@@ -235,7 +235,8 @@ def test_blur_paths_1080p_and_8k_planes(siftgpu, oracle, monkeypatch, mode):
     """Every blur path at full size against the CPU path's plane digests: the
     scatter walk's multi-chunk plans (a 1080p or 8K image is split into
     chunks per scale), the same in XCD-contiguous wave order
-    (SIFT_HIP_SYM_XCD=1, padding blocks included), the 2-D 8-pixel tiles, and
+    (SIFT_HIP_SYM_XCD=1, padding blocks included; the default since round 5, so
+    "sym" forces the launch order with SIFT_HIP_SYM_XCD=0), the 2-D 8-pixel tiles, and
     the 2-output tiles of small launches (blur_small_kernel) forced onto every
     octave."""
     monkeypatch.setenv("SIFT_HIP_SYM_XCD", "1" if mode == "sym_xcd" else "0")
