@@ -106,38 +106,61 @@ __device__ __forceinline__ float exp32f(float v, const float* __restrict__ tab,
   if (CLAMP) {
     v = v < k.lo ? k.lo : v;
     v = k.hi < v ? k.hi : v;
+    v = v * k.prescale;
+    int vi = cv_round(v);
+    v = (v - (float)vi) * k.post;
+    int t = (vi >> 6) + 127;
+    t = !(t & ~255) ? t : t < 0 ? 0 : 255;
+    float sc = __int_as_float(t << 23);
+    float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
+    return sc * tab[vi & 63] * poly;
+  } else {
+    // see exp32f_v: same bits inside the argument range the callers state
+    v = v * k.prescale;
+    const float r = rintf(v);  // cv_round's value, kept as a float
+    const int vi = (int)r;
+    v = (v - r) * k.post;
+    float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
+    return __builtin_amdgcn_ldexpf(tab[vi & 63], vi >> 6) * poly;
   }
-  v = v * k.prescale;
-  int vi = cv_round(v);
-  v = (v - (float)vi) * k.post;
-  int t = (vi >> 6) + 127;
-  t = !(t & ~255) ? t : t < 0 ? 0 : 255;
-  float sc = __int_as_float(t << 23);
-  float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
-  return sc * tab[vi & 63] * poly;
 }
 
 // The same with the table held one entry per lane (lane j: tab[j]) and read
 // with a cross-lane permute instead of an LDS gather; every lane of the wave
 // must execute it.
-// CLAMP = false drops exp32f's input clamp to [lo, hi]: exact for callers whose
-// argument is known to lie inside it (the descriptor's -(c^2 + r^2) / 8 over a
-// window), and still finite outside it (t is clamped below).
+// CLAMP = false is for callers whose argument lies in (-87, 0] (the
+// descriptor's -(c^2 + r^2) / 8 over a window: > -1.6; the orientation's:
+// > -36): exp32f's input clamp to [lo, hi] never acts there, and the exponent
+// t = (vi >> 6) + 127 stays in [1, 127], so its clamp to [0, 255] does not
+// act either and 2^(vi >> 6) * tab[...] is an exact power-of-two scaling of a
+// normal float -- one v_ldexp_f32 gives the same bits as building the scale
+// and multiplying.  (float)cv_round(v) is rintf(v) for |v| < 2^24, so the
+// rounded value is kept as a float.  Outside that range the result is
+// finite garbage (callers mask it).  The lane permute uses address bits [7:2]
+// only, so vi << 2 indexes lane vi & 63.
 template <bool CLAMP = true>
 __device__ __forceinline__ float exp32f_v(float v, float tab_lane, const ExpConsts& k) {
   if (CLAMP) {
     v = v < k.lo ? k.lo : v;
     v = k.hi < v ? k.hi : v;
+    v = v * k.prescale;
+    int vi = cv_round(v);
+    v = (v - (float)vi) * k.post;
+    int t = (vi >> 6) + 127;
+    t = !(t & ~255) ? t : t < 0 ? 0 : 255;
+    float sc = __int_as_float(t << 23);
+    float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
+    const float tv = __int_as_float(__builtin_amdgcn_ds_bpermute((vi & 63) << 2, __float_as_int(tab_lane)));
+    return sc * tv * poly;
+  } else {
+    v = v * k.prescale;
+    const float r = rintf(v);
+    const int vi = (int)r;
+    v = (v - r) * k.post;
+    float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
+    const float tv = __int_as_float(__builtin_amdgcn_ds_bpermute(vi << 2, __float_as_int(tab_lane)));
+    return __builtin_amdgcn_ldexpf(tv, vi >> 6) * poly;
   }
-  v = v * k.prescale;
-  int vi = cv_round(v);
-  v = (v - (float)vi) * k.post;
-  int t = (vi >> 6) + 127;
-  t = !(t & ~255) ? t : t < 0 ? 0 : 255;
-  float sc = __int_as_float(t << 23);
-  float poly = (((v + k.A1) * v + k.A2) * v + k.A3) * v + k.A4;
-  const float tv = __int_as_float(__builtin_amdgcn_ds_bpermute((vi & 63) << 2, __float_as_int(tab_lane)));
-  return sc * tv * poly;
 }
 
 // hal::fastAtan2 in degrees.

@@ -247,6 +247,7 @@ descriptor_kernel(DescArgs A) {
     nmax = max(nmax, __shfl_xor(nmax, 8));
     nmax = max(nmax, __shfl_xor(nmax, 16));
     nmax = max(nmax, __shfl_xor(nmax, 32));
+    nmax = __builtin_amdgcn_readfirstlane(nmax);  // wave-uniform: scalar loop control
     wave_sync_d();
     // lane q walks candidate samples t = q, q+8, ... in raster order (row ri, offset u)
     int ri = 0, u = q, rlo = -radius, rlen = D;
@@ -316,16 +317,32 @@ descriptor_kernel(DescArgs A) {
     auto finish = [&](const Loc& L, RecT<PACKED>& out, int& odd_out) {
       const float rbin = L.rbin, cbin = L.cbin;
       const bool ok = L.ok;
-      // invalid: (0, 0) -- border gradients are never written and may hold NaN
-      const float2 mo = ok ? L.mo_raw : make_float2(0.f, 0.f);
+      // An invalid sample must add +0.0 everywhere.  Caller keypoints: its
+      // pixel is (0, 0) -- it gathered the clamped centre, and border
+      // gradients are never written and may hold NaN.  Detected keypoints
+      // (DET) lie >= SIFT_IMG_BORDER inside the image, so the centre's
+      // gradient is finite and a zero weight alone makes mag = +0 (one select
+      // instead of two); lanes of an inactive group may sum NaN into their
+      // own histogram, which is never stored.
+      const float2 mo = DET || ok ? L.mo_raw : make_float2(0.f, 0.f);
       float obin = (mo.y - ori) * bins_per_rad;
-      const float mag = mo.x * L.w;
+      const float mag = mo.x * (!DET || ok ? L.w : 0.f);
       const float fo = floorf(obin);  // |obin| < 10: exact, as above
       int o0 = (int)fo;
       obin -= fo;
-      if (o0 < 0) o0 += nb;
-      if (o0 >= nb) o0 -= nb;
-      const int Rm = L.Rm, Cm = L.Cm, O0 = ok ? o0 : 0;
+      int O0;
+      if constexpr (DET) {
+        // Ori in [0, 360] and ori in [0, 360) put obin in (-8, 8], so o0 in
+        // [-8, 8], where the two wraps below are o0 & 7 (nb = 8); an invalid
+        // sample's o0 is any bin (its values are +0.0)
+        static_assert(kDescBins == 8, "o0 & 7 is the wrap for 8 bins");
+        O0 = o0 & 7;
+      } else {
+        if (o0 < 0) o0 += nb;
+        if (o0 >= nb) o0 -= nb;
+        O0 = ok ? o0 : 0;
+      }
+      const int Rm = L.Rm, Cm = L.Cm;
       const int odd = ((Rm & 1) << 2) | ((Cm & 1) << 1) | (O0 & 1);
       float v_r1 = mag * rbin, v_r0 = mag - v_r1;
       if constexpr (PACKED) {
