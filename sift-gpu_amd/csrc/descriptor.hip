@@ -50,6 +50,7 @@ constexpr int kChunk = 64;         // keypoints ranked together by window radius
 constexpr int kQBins = 21;         // bins per parity class: 2 x 2 x 5 interior + 1 trash
 constexpr int kTrash = 20;         // qidx of the discarded border bins
 constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
+constexpr int kRowsTab = kMaxWinRows + 2;  // + the entries D, D + 1 the walk reads past its last row (unused values)
 constexpr int kRecStride2 = 132;   // words per sample row of the owner records (128 + pad)
 
 struct DescArgs {
@@ -127,7 +128,7 @@ descriptor_kernel(DescArgs A) {
   // words hold the sub-batch's keypoint indices and the normalisation scalars
   __shared__ __attribute__((aligned(16))) float rec[PACKED ? kGrp * kRecG : 8 * kRecStride2];
   // per row: (jlo + 64) | len << 16 (PACKED: << 8, 16 bits)
-  __shared__ typename std::conditional<PACKED, unsigned short, int>::type rows_tab[kGrp][kMaxWinRows];
+  __shared__ typename std::conditional<PACKED, unsigned short, int>::type rows_tab[kGrp][kRowsTab];
   constexpr int kLenSh = PACKED ? 8 : 16, kLoMask = PACKED ? 0xff : 0xffff;
   int* const sord = reinterpret_cast<int*>(rec);                 // [kGrp] keypoint indices
   float(*const bc)[4] = reinterpret_cast<float(*)[4]>(rec + kGrp);  // [kGrp][4] normalisation scalars
@@ -243,6 +244,7 @@ descriptor_kernel(DescArgs A) {
       nsamp = D * D;  // radius > 40 (caller-supplied keypoints): the whole window
     }
     for (int t = 0; t < kHistRows; ++t) hist[t * 64 + lane] = 0.f;
+    const int nsq = nsamp - q;  // sample base + q is in range iff base < nsq
     int nmax = nsamp;
     nmax = max(nmax, __shfl_xor(nmax, 8));
     nmax = max(nmax, __shfl_xor(nmax, 16));
@@ -419,7 +421,12 @@ descriptor_kernel(DescArgs A) {
     // ahead), so the common advance -- at most one row change -- is
     // branch-free selects with no LDS round trip; short or empty rows fall
     // back to the row walk under a wave-uniform branch.
-    int enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
+    // DET: ri <= D <= kMaxWinRows, so entry ri + 1 lies in the table; entries
+    // D and D + 1 are never written and only reach rlo / rlen once ri == D,
+    // when no sample is in range any more.  Caller keypoints may have D >
+    // kMaxWinRows (no table, the value is unused): clamped.
+    auto next_entry = [&]() { return rows_tab[g][DET ? ri + 1 : min(ri + 1, kRowsTab - 1)]; };
+    int enext = next_entry();
     auto advance = [&]() {  // to candidate sample t + 8
       u += 8;
       const bool mv = ri < D && u >= rlen;
@@ -437,7 +444,7 @@ descriptor_kernel(DescArgs A) {
           rlen = e >> kLenSh;
         }
       }
-      enext = rows_tab[g][min(ri + 1, kMaxWinRows - 1)];
+      enext = next_entry();
     };
     int odd_cur = 0;
     uint2 qq_cur = make_uint2(0u, 0u);  // PACKED: this owner's 8 bin bytes of the batch
@@ -445,13 +452,13 @@ descriptor_kernel(DescArgs A) {
     if (nmax > 0) {
       if constexpr (PF == 2) {
         Loc l0;
-        locate(q < nsamp, l0);
+        locate(0 < nsq, l0);
         advance();
-        locate(8 + q < nsamp, loc_nxt);
+        locate(8 < nsq, loc_nxt);
         advance();
         finish(l0, rc_cur, odd_cur);
       } else {
-        sample(q < nsamp, rc_cur, odd_cur);
+        sample(0 < nsq, rc_cur, odd_cur);
         advance();
       }
     }
@@ -508,11 +515,11 @@ descriptor_kernel(DescArgs A) {
       RecT<PACKED> rc_nxt;
       int odd_nxt = 0;
       if constexpr (PF == 2) {
-        locate(base + 16 + q < nsamp, l2);  // batch k + 2: its gather flies for two steps
+        locate(base + 16 < nsq, l2);  // batch k + 2: its gather flies for two steps
         advance();
         finish(ln, rc_nxt, odd_nxt);
       } else {
-        locate(base + 8 + q < nsamp, l2);  // batch k + 1: finished after this batch's chain
+        locate(base + 8 < nsq, l2);  // batch k + 1: finished after this batch's chain
       }
       // ordered accumulation of batch k: lane q applies its record of each sample
       if constexpr (PACKED) {

@@ -1306,11 +1306,10 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
       if (base + 64 < ns) gather(base + 64, ok_n, mo_n);
       // |argument| <= 2 * 17^2 / (2 * 2.85^2) < 36: exp32f's input clamp never acts
       const float wgt = exp32f_v<false>((i * i + j * j) * escale, etab_lane, ek);
-      int bin = cv_round((kOriBins / 360.f) * mo.y);
-      if (bin >= kOriBins) bin -= kOriBins;
-      if (bin < 0) bin += kOriBins;
+      // Ori in [0, 360]: bin in [0, 36], the reference's wraps reduce to 36 -> 0
+      const int bin = cv_round((kOriBins / 360.f) * mo.y);
       const float val = wgt * mo.x;
-      const int key = ok ? bin : 63;
+      const int key = ok ? (bin != kOriBins ? bin : 0) : 63;
       // lanes with the same key: match over the key's 6 bits
       unsigned long long m = ~0ull;
 #pragma unroll
@@ -1528,11 +1527,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2
 #pragma unroll
       for (int u = 0; u < kOSlots; ++u) {
         // src/sift.cpp:426-432: Ori = fastAtan2 (precomputed), bin, W * Mag
-        int bn = cv_round((kOriBins / 360.f) * mo[u].y);
-        if (bn >= kOriBins) bn -= kOriBins;
-        if (bn < 0) bn += kOriBins;
+        // Ori in [0, 360] (fastAtan2 of this library's gradients) puts bn in
+        // [0, 36]: the reference's two wraps reduce to 36 -> 0, folded into
+        // the validity select
+        const int bn = cv_round((kOriBins / 360.f) * mo[u].y);
         const bool okv = wt[u] > 0.f;
-        bin[u] = okv ? bn : 0;
+        bin[u] = okv && bn != kOriBins ? bn : 0;
         val[u] = okv ? wt[u] * mo[u].x : 0.f;
       }
       if (base + 8 < nmax) fetch(base + 8);  // next batch's gathers fly during this chain
