@@ -127,8 +127,9 @@ descriptor_kernel(DescArgs A) {
   // per-sample hand-off records (see RecT); outside the sample loop the same
   // words hold the sub-batch's keypoint indices and the normalisation scalars
   __shared__ __attribute__((aligned(16))) float rec[PACKED ? kGrp * kRecG : 8 * kRecStride2];
-  // per row: (jlo + 64) | len << 16 (PACKED: << 8, 16 bits)
-  __shared__ typename std::conditional<PACKED, unsigned short, int>::type rows_tab[kGrp][kRowsTab];
+  // per row: (jlo + 64) | len << 16 (PACKED: << 8, 16 bits); DET: (jb << 16) | cum
+  // (see the walk below)
+  __shared__ typename std::conditional<PACKED && !DET, unsigned short, int>::type rows_tab[kGrp][kRowsTab];
   constexpr int kLenSh = PACKED ? 8 : 16, kLoMask = PACKED ? 0xff : 0xffff;
   int* const sord = reinterpret_cast<int*>(rec);                 // [kGrp] keypoint indices
   float(*const bc)[4] = reinterpret_cast<float(*)[4]>(rec + kGrp);  // [kGrp][4] normalisation scalars
@@ -226,7 +227,44 @@ descriptor_kernel(DescArgs A) {
     const bool table = DET || D <= kMaxWinRows;
     // ---- per-row candidate j-ranges and the sample count ----
     int nsamp = 0;
-    if (table) {
+    if constexpr (DET) {
+      // Lane q takes the contiguous rows [r0, r1) (ceil(D / 8) each): per row
+      // its candidate j-range [lo, lo + len), then, after a prefix sum of the
+      // counts over the group, the entry (jb << 16) | cum with cum = the
+      // candidates before the row and jb = lo - cum, so candidate t of the
+      // group's raster-ordered list lies in the row whose cum <= t < next cum,
+      // at j = t + jb.  Two sentinel entries (cum = 0xffff) follow row D - 1.
+      const int rb = (D + 7) >> 3;
+      const int r0 = min(q * rb, D), r1 = min(r0 + rb, D);
+      int cnt = 0;
+      for (int ri = r0; ri < r1; ++ri) {
+        const int i = ri - radius;
+        int lo = max(-radius, 1 - px), hi = min(radius, cols - 2 - px);  // 0 < px + j < cols-1
+        if (!(py + i > 0 && py + i < rows - 1)) hi = lo - 1;
+        slab(sin_t, inv_sin, i * cos_t, lo, hi);     // r_rot = j*sin_t + i*cos_t
+        slab(cos_t, inv_cos, -(i * sin_t), lo, hi);  // c_rot = j*cos_t - i*sin_t
+        const int len = hi >= lo ? hi - lo + 1 : 0;
+        rows_tab[g][ri] = (int)(((unsigned)lo << 16) | (unsigned)len);  // |lo| <= 40
+        cnt += len;
+      }
+      int incl = cnt;
+#pragma unroll
+      for (int sh = 1; sh < 8; sh <<= 1) {
+        const int y = __shfl_up(incl, sh, 8);
+        if (q >= sh) incl += y;
+      }
+      nsamp = __shfl(incl, 7, 8);  // <= 81 * 81
+      int cum = incl - cnt;
+      for (int ri = r0; ri < r1; ++ri) {
+        const int e = rows_tab[g][ri];
+        rows_tab[g][ri] = (int)(((unsigned)((e >> 16) - cum) << 16) | (unsigned)cum);
+        cum += e & 0xffff;
+      }
+      if (q == 7) {
+        rows_tab[g][D] = 0xffff;
+        rows_tab[g][D + 1] = 0xffff;
+      }
+    } else if (table) {
       for (int ri = q; ri < D; ri += 8) {
         const int i = ri - radius;
         int lo = max(-radius, 1 - px), hi = min(radius, cols - 2 - px);  // 0 < px + j < cols-1
@@ -253,12 +291,24 @@ descriptor_kernel(DescArgs A) {
     wave_sync_d();
     // lane q walks candidate samples t = q, q+8, ... in raster order (row ri, offset u)
     int ri = 0, u = q, rlo = -radius, rlen = D;
-    if (table && D > 0) {
+    // DET: the walk holds t and the table entries of rows ri, ri + 1, ri + 2
+    int t = q, e0 = 0, e1 = 0, e2 = 0;
+    if constexpr (DET) {
+      e0 = rows_tab[g][0];
+      e1 = rows_tab[g][1];
+      while (t >= (e1 & 0xffff)) {  // stops at the sentinel (row D) at the latest
+        ++ri;
+        e0 = e1;
+        e1 = rows_tab[g][ri + 1];
+      }
+      e2 = rows_tab[g][ri + 2];
+      rlen = 0;  // unused
+    } else if (table && D > 0) {
       const int e = rows_tab[g][0];
       rlo = (e & kLoMask) - 64;
       rlen = e >> kLenSh;
     }
-    while (ri < D && u >= rlen) {
+    while (!DET && ri < D && u >= rlen) {
       u -= rlen;
       if (++ri < D && table) {
         const int e = rows_tab[g][ri];
@@ -288,33 +338,46 @@ descriptor_kernel(DescArgs A) {
     // (weight, spatial bins); finish: the rest.
     struct Loc {
       float w, rbin, cbin;  // Gaussian weight; fractional spatial bin parts
-      int Rm, Cm;           // interior base corner (0 for an invalid sample)
+      int X, Y;             // base corner + 1: X = Rm + 1 = cvFloor(rbin) + 1 in [0, d] (1 for an invalid sample)
       float2 mo_raw;
       bool ok;
     };
     auto locate = [&](bool in_range, Loc& L) {
-      const int i = ri - radius, j = rlo + u;
+      const int i = ri - radius, j = DET ? t + (e0 >> 16) : rlo + u;
       const float c_rot = j * cos_t - i * sin_t;
       const float r_rot = j * sin_t + i * cos_t;
       float rbin = r_rot + d / 2 - 0.5f;
       float cbin = c_rot + d / 2 - 0.5f;
       const int r = py + i, c = px + j;
-      // the row table enumerates interior pixels only (src/sift.cpp:620-621's
-      // 0 < r < rows-1, 0 < c < cols-1), so only the whole-window walk tests them
-      L.ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d &&
-             (table || (r > 0 && r < rows - 1 && c > 0 && c < cols - 1));
-      // an invalid sample gathers from the clamped keypoint centre (any valid
-      // address: its value is replaced below); plane offsets fit 32 bits
-      L.mo_raw = gimg[(unsigned)(L.ok ? __mul24(r, pitch32) + c : ctr_off)];  // (Mag, Ori) of the pixel
-      L.w = exp32f_v<false>((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
       // cvFloor: |rbin|, |cbin| < 10, so floorf is exact and (int)floorf ==
       // cvFloor; rbin - floorf(rbin) == rbin - (float)r0
       const float fr = floorf(rbin), fc = floorf(cbin);
+      const int xr = (int)fr + 1, yc = (int)fc + 1;
+      // the row table enumerates interior pixels only (src/sift.cpp:620-621's
+      // 0 < r < rows-1, 0 < c < cols-1), so only the whole-window walk tests them.
+      // DET tests rbin, cbin in (-1, d) as cvFloor in [-1, d - 1]: that admits
+      // rbin (cbin) == -1.0 exactly, a sample whose every corner value is +0.0
+      // (the R = -1 corners are masked, the R = 0 ones carry mag * 0), an
+      // exact no-op; two integer compares instead of four float ones
+      if constexpr (DET)
+        L.ok = in_range && (unsigned)xr <= (unsigned)d && (unsigned)yc <= (unsigned)d;
+      else
+        L.ok = in_range && rbin > -1 && rbin < d && cbin > -1 && cbin < d &&
+               (table || (r > 0 && r < rows - 1 && c > 0 && c < cols - 1));
+      // an invalid sample gathers from the clamped keypoint centre (any valid
+      // address: its value is replaced below); plane offsets fit 32 bits
+      int pix = __mul24(r, pitch32) + c;
+      if constexpr (DET) asm volatile("" : "+v"(pix));  // computed on every lane: a select, not a branch
+      L.mo_raw = gimg[(unsigned)(L.ok ? pix : ctr_off)];  // (Mag, Ori) of the pixel
+      L.w = exp32f_v<false>((c_rot * c_rot + r_rot * r_rot) * exp_scale, etab_lane, ek);
       L.rbin = rbin - fr;
       L.cbin = cbin - fc;
-      // interior coordinates of the base corner: Rm = R0 - 1 = r0 in [-1, 3]
-      L.Rm = L.ok ? (int)fr : 0;
-      L.Cm = L.ok ? (int)fc : 0;
+      // the base corner R0 = r0 + 1 = X in [0, d] (interior coordinate Rm =
+      // X - 1 in [-1, 3]); an invalid sample's values are all +0.0, so any
+      // base corner serves it: DET clamps, which keeps the perm-table
+      // selectors in range without waiting for ok
+      L.X = DET ? min(max(xr, 0), d) : L.ok ? xr : 1;
+      L.Y = DET ? min(max(yc, 0), d) : L.ok ? yc : 1;
     };
     auto finish = [&](const Loc& L, RecT<PACKED>& out, int& odd_out) {
       const float rbin = L.rbin, cbin = L.cbin;
@@ -344,7 +407,7 @@ descriptor_kernel(DescArgs A) {
         if (o0 >= nb) o0 -= nb;
         O0 = ok ? o0 : 0;
       }
-      const int Rm = L.Rm, Cm = L.Cm;
+      const int X = L.X, Y = L.Y, Rm = X - 1, Cm = Y - 1;  // Rm, Cm: the unpacked form only
       const int odd = ((Rm & 1) << 2) | ((Cm & 1) << 1) | (O0 & 1);
       float v_r1 = mag * rbin, v_r0 = mag - v_r1;
       if constexpr (PACKED) {
@@ -352,16 +415,16 @@ descriptor_kernel(DescArgs A) {
         // bin: an exact no-op, every bin is >= +0) instead of going to a
         // trash bin; each weight is masked after every product that uses its
         // unmasked value, so the interior corners' values are unchanged
-        v_r0 = Rm >= 0 ? v_r0 : 0.f;
-        v_r1 = Rm <= 2 ? v_r1 : 0.f;
+        v_r0 = X >= 1 ? v_r0 : 0.f;  // Rm >= 0
+        v_r1 = X <= 3 ? v_r1 : 0.f;  // Rm <= 2
       }
       float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
       float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
       if constexpr (PACKED) {  // and outside the interior columns
-        v_rc00 = Cm >= 0 ? v_rc00 : 0.f;
-        v_rc10 = Cm >= 0 ? v_rc10 : 0.f;
-        v_rc01 = Cm <= 2 ? v_rc01 : 0.f;
-        v_rc11 = Cm <= 2 ? v_rc11 : 0.f;
+        v_rc00 = Y >= 1 ? v_rc00 : 0.f;
+        v_rc10 = Y >= 1 ? v_rc10 : 0.f;
+        v_rc01 = Y <= 3 ? v_rc01 : 0.f;
+        v_rc11 = Y <= 3 ? v_rc11 : 0.f;
       }
       float v[8];
       v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
@@ -386,7 +449,7 @@ descriptor_kernel(DescArgs A) {
         // their entries for a row / column outside the interior are arbitrary
         // interior bins (those corners carry +0.0, above).
         // (byte replication by v_perm_b32 with selector 0)
-        const unsigned x = (unsigned)(Rm + 1), y = (unsigned)(Cm + 1);
+        const unsigned x = (unsigned)X, y = (unsigned)Y;
         const unsigned selR1 = __builtin_amdgcn_perm(0u, x, 0u), selR0 = selR1 + 0x01010101u;
         const unsigned selC = __builtin_amdgcn_perm(0u, y, 0u) + 0x00000101u;
         const unsigned po = (unsigned)(O0 & 1);
@@ -410,7 +473,10 @@ descriptor_kernel(DescArgs A) {
           out.r[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
                                  v[2 * t + 1]);
       }
-      odd_out = odd;
+      // PACKED: the slot bits of the hand-off store address from the parities
+      // of X = Rm + 1 and Y = Cm + 1 -- (odd ^ 6) << 5, i.e. slot s is stored
+      // at position s ^ 6 (the owner reads there) -- by shift-and-or steps
+      odd_out = PACKED ? ((X << 7) & 0x80) | ((Y << 6) & 0x40) | ((O0 & 1) << 5) : odd;
     };
     auto sample = [&](bool in_range, RecT<PACKED>& out, int& odd_out) {
       Loc L;
@@ -421,30 +487,45 @@ descriptor_kernel(DescArgs A) {
     // ahead), so the common advance -- at most one row change -- is
     // branch-free selects with no LDS round trip; short or empty rows fall
     // back to the row walk under a wave-uniform branch.
-    // DET: ri <= D <= kMaxWinRows, so entry ri + 1 lies in the table; entries
-    // D and D + 1 are never written and only reach rlo / rlen once ri == D,
-    // when no sample is in range any more.  Caller keypoints may have D >
-    // kMaxWinRows (no table, the value is unused): clamped.
-    auto next_entry = [&]() { return rows_tab[g][DET ? ri + 1 : min(ri + 1, kRowsTab - 1)]; };
-    int enext = next_entry();
+    // Caller keypoints may have D > kMaxWinRows (no table, the value is
+    // unused): clamped.
+    auto next_entry = [&]() { return rows_tab[g][min(ri + 1, kRowsTab - 1)]; };
+    int enext = DET ? 0 : next_entry();
     auto advance = [&]() {  // to candidate sample t + 8
-      u += 8;
-      const bool mv = ri < D && u >= rlen;
-      u = mv ? u - rlen : u;
-      ri = mv ? ri + 1 : ri;
-      if (table) {
-        rlo = mv ? (enext & kLoMask) - 64 : rlo;
-        rlen = mv ? enext >> kLenSh : rlen;
-      }
-      while (ri < D && u >= rlen) {  // skipped by exec when no lane needs it
-        u -= rlen;
-        if (++ri < D && table) {
-          const int e = rows_tab[g][ri];
-          rlo = (e & kLoMask) - 64;
-          rlen = e >> kLenSh;
+      if constexpr (DET) {
+        // entries e1, e2 of rows ri + 1, ri + 2 were loaded an advance ahead:
+        // a move by one row is compares and selects; rows shorter than 8 take
+        // the loop (the sentinel after row D - 1 ends it)
+        t += 8;
+        const bool mv = t >= (e1 & 0xffff);
+        ri += mv ? 1 : 0;
+        e0 = mv ? e1 : e0;
+        e1 = mv ? e2 : e1;
+        while (t >= (e1 & 0xffff)) {
+          ++ri;
+          e0 = e1;
+          e1 = rows_tab[g][ri + 1];
         }
+        e2 = rows_tab[g][ri + 2];  // ri <= D - 1: within the table
+      } else {
+        u += 8;
+        const bool mv = ri < D && u >= rlen;
+        u = mv ? u - rlen : u;
+        ri = mv ? ri + 1 : ri;
+        if (table) {
+          rlo = mv ? (enext & kLoMask) - 64 : rlo;
+          rlen = mv ? enext >> kLenSh : rlen;
+        }
+        while (ri < D && u >= rlen) {  // skipped by exec when no lane needs it
+          u -= rlen;
+          if (++ri < D && table) {
+            const int e = rows_tab[g][ri];
+            rlo = (e & kLoMask) - 64;
+            rlen = e >> kLenSh;
+          }
+        }
+        enext = next_entry();
       }
-      enext = next_entry();
     };
     int odd_cur = 0;
     uint2 qq_cur = make_uint2(0u, 0u);  // PACKED: this owner's 8 bin bytes of the batch
@@ -466,7 +547,7 @@ descriptor_kernel(DescArgs A) {
     // located in this step
     auto step = [&](int base, Loc& ln, Loc& l2) {
       if constexpr (PACKED) {
-        // corner k to owner slot s = k ^ odd: value at byte (g << 8) | (s << 5) |
+        // corner k to owner slot s = k ^ odd: value at byte (g << 8) | ((s ^ 6) << 5) |
         // (q << 2), bit 4 flipped on odd groups (so a 16-lane pass of the
         // owners' ds_read_b128 -- an even and an odd group -- covers all 64
         // banks); bin byte at (g << 6) | (s << 3) | q.  Slot bits are clear
@@ -477,7 +558,7 @@ descriptor_kernel(DescArgs A) {
         // swizzle costs ~3 VALU per batch and the kernel took 7.57-7.69 vs
         // 7.45-7.47 ms: it is bound by VALU issue, not by the conflicts.)
         char* rb = reinterpret_cast<char*>(rec);
-        const int wv = ((g << 8) | ((q << 2) ^ ((g & 1) << 4))) | (odd_cur << 5);
+        const int wv = ((g << 8) | ((q << 2) ^ ((g & 1) << 4))) | odd_cur;  // odd_cur = odd << 5
 #pragma unroll
         for (int k = 0; k < 8; ++k) *reinterpret_cast<float*>(rb + (wv ^ (k << 5))) = rc_cur.v[k];
         // bin bytes to their owners in registers (round 4; were eight
@@ -524,7 +605,7 @@ descriptor_kernel(DescArgs A) {
       // ordered accumulation of batch k: lane q applies its record of each sample
       if constexpr (PACKED) {
         const char* rb = reinterpret_cast<const char*>(rec);
-        const int rv = (g << 8) | (q << 5);  // samples 0-3 at bit 4 = g & 1, samples 4-7 at the other half
+        const int rv = (g << 8) | ((q ^ 6) << 5);  // slot q at position q ^ 6 (finish's odd_out)  // samples 0-3 at bit 4 = g & 1, samples 4-7 at the other half
         const float4 va = *reinterpret_cast<const float4*>(rb + (rv | ((g & 1) << 4)));
         const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | (((g & 1) ^ 1) << 4)));
         const uint2 qq = qq_cur;
