@@ -767,9 +767,14 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
     const char* e = getenv("SIFT_HIP_DESC_DEEP");
     return !e || atoi(e) != 0;
   }();
+#ifndef SIFT_DESC_GRID_PCT
+#define SIFT_DESC_GRID_PCT 100  // A/B builds only (tools/build_var.sh): the grid as a share of the resident one
+#endif
 #define SIFT_DESC_LAUNCH(...)                                                                                       \
   hipLaunchKernelGGL((descriptor_kernel<__VA_ARGS__>),                                                              \
-                     dim3(resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192)), dim3(64), 0, st, A)
+                     dim3(std::max(8, resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192) *     \
+                                          SIFT_DESC_GRID_PCT / 800 * 8)),                                           \
+                     dim3(64), 0, st, A)
   if (packed && detected && deep && one_image_variants(L, batch))
     SIFT_DESC_LAUNCH(true, true, 2, 2);
   else if (packed && detected && deep)
