@@ -1274,24 +1274,31 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
     const float sigma = 1.5f * scl;
     const float escale = -1.f / (2.f * sigma * sigma);
     const float2* gwin = A.grad + co.img * A.L.g_img + O.g_off[co.ref_layer];
-    const int D = 2 * radius + 1, ns = D * D;
-    // lane's sample index base + lane as (si, sj) of the D x D window, moved
-    // on by 64 = q D + rem per batch
-    int si = lane / D, sj = lane - (lane / D) * D;
-    const int q64 = 64 / D, r64 = 64 - q64 * D;
+    const int D = 2 * radius + 1;
+    // the window's valid rectangle (y in [1, rows - 2], x in [1, cols - 2],
+    // src/sift.cpp:405,410): the pixels the reference skips are not
+    // enumerated, so the rest keep their raster order and a sample needs no
+    // range test; a kept candidate lies >= 5 px inside, so it is >= 14 wide
+    const int i0 = max(0, 1 - rr + radius), i1 = min(D - 1, O.rows - 2 - rr + radius);
+    const int j0 = max(0, 1 - rc + radius), j1 = min(D - 1, O.cols - 2 - rc + radius);
+    const int W = max(j1 - j0 + 1, 1), ns = max(j1 - j0 + 1, 0) * max(i1 - i0 + 1, 0);
+    // lane's sample index base + lane as (si, sj) of the window, moved on by
+    // 64 = q W + rem per batch
+    int si = i0 + lane / W, sj = j0 + lane - (lane / W) * W;
+    const int q64 = 64 / W, r64 = 64 - q64 * W, jend = j0 + W;
     float acc = 0.f;  // lane b < 36: bin b's running sum
     // the batch at (si, sj): validity and the gather (issued one batch ahead,
     // so its latency runs under the previous batch's bucketing)
     auto gather = [&](int base_, bool& ok_, float2& mo_) {
       const int y = rr + si - radius, x = rc + sj - radius;
-      ok_ = base_ + lane < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
+      ok_ = base_ + lane < ns;
       mo_ = gwin[ok_ ? (long long)y * pitch + x : (long long)rr * pitch + rc];  // (Mag, Ori)
     };
     auto step64 = [&]() {
       si += q64;
       sj += r64;
-      if (sj >= D) {
-        sj -= D;
+      if (sj >= jend) {
+        sj -= W;
         ++si;
       }
     };
@@ -1437,11 +1444,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2
       if (rank >= win && rank < win + SB) sord[rank - win] = kk;
       wave_sync();
     }
-    // per slot: the window's top-left gradient address (gwin, pitch), the
-    // sample walk (si, sj) over D x D, and the valid range of (si, sj) --
-    // interior pixels only, src/sift.cpp:405,410 -- as [lo, hi] bounds
-    int radius[kOSlots], ns[kOSlots], Dw[kOSlots], si[kOSlots], sj[kOSlots], pitch[kOSlots], ilo[kOSlots],
-        ihi[kOSlots], jlo[kOSlots], jhi[kOSlots];
+    // per slot: the window's top-left gradient address (gwin, pitch) and the
+    // sample walk (si, sj) over the window's valid rectangle -- interior
+    // pixels only, src/sift.cpp:405,410, the pixels the reference skips are
+    // never enumerated, so the raster order of the rest is unchanged and a
+    // sample needs no per-pixel range test: [j0, jend) x rows from si
+    int radius[kOSlots], ns[kOSlots], Dw[kOSlots], si[kOSlots], sj[kOSlots], pitch[kOSlots], jend[kOSlots];
     float escale[kOSlots];
     const float2* gwin[kOSlots];
     int nmax = 0;
@@ -1473,16 +1481,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2
       // border), so the window centre is a valid address for every slot
       gwin[u] = A.grad + b * A.L.g_img + O.g_off[ok ? rl : 0] + (long long)(rr - rad) * pitch[u] + (rc - rad);
       const int D = 2 * rad + 1;
-      ns[u] = ok ? D * D : 0;
-      Dw[u] = ns[u] ? D : 0x40000000;  // rejected: never wraps
-      ilo[u] = 1 - rr + rad;           // y = rr + si - rad in [1, rows - 2]
-      ihi[u] = O.rows - 2 - rr + rad;
-      jlo[u] = 1 - rc + rad;
-      jhi[u] = O.cols - 2 - rc + rad;
-      // lane q walks samples s = q, q+8, ... as (row si, column sj) of the window
-      si[u] = 0;
-      sj[u] = q;
-      while (sj[u] >= Dw[u]) {
+      // y = rr + si - rad in [1, rows - 2], x = rc + sj - rad in [1, cols - 2]
+      const int i0 = max(0, 1 - rr + rad), i1 = min(D - 1, O.rows - 2 - rr + rad);
+      const int j0 = max(0, 1 - rc + rad), j1 = min(D - 1, O.cols - 2 - rc + rad);
+      const int wv = j1 - j0 + 1, hv = i1 - i0 + 1;
+      ns[u] = ok && wv > 0 && hv > 0 ? wv * hv : 0;
+      // a kept candidate lies >= 5 px inside its octave and rad >= 9, so wv >= 14
+      // > 8: one advance wraps at most once; rejected: never wraps
+      Dw[u] = ns[u] ? wv : 0x40000000;
+      jend[u] = ns[u] ? j1 + 1 : 0x40000000;
+      // lane q walks samples s = q, q+8, ... as (row si, column sj) of the rectangle
+      si[u] = i0;
+      sj[u] = j0 + q;
+      while (sj[u] >= jend[u]) {
         sj[u] -= Dw[u];
         ++si[u];
       }
@@ -1506,15 +1517,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2
 #pragma unroll
       for (int u = 0; u < kOSlots; ++u) {
         const int i = si[u] - radius[u], j = sj[u] - radius[u];
-        const bool okv = base + q < ns[u] && si[u] >= ilo[u] && si[u] <= ihi[u] && sj[u] >= jlo[u] &&
-                         sj[u] <= jhi[u];
+        const bool okv = base + q < ns[u];
         // 24-bit products, 32-bit offsets (full-rate VALU; a window's offsets are < 2^31)
         mo[u] = gwin[u][(unsigned)(okv ? __mul24(si[u], pitch[u]) + sj[u] : __mul24(radius[u], pitch[u] + 1))];  // (Mag, Ori)
         // |argument| <= 2 * 17^2 / (2 * 2.85^2) < 36: exp32f's input clamp never acts
         const float w = exp32f<false>((__mul24(i, i) + __mul24(j, j)) * escale[u], etab, ek);
         wt[u] = okv ? w : -1.f;
-        sj[u] += 8;  // D >= 19 > 8 for every kept candidate: at most one wrap
-        if (sj[u] >= Dw[u]) {
+        sj[u] += 8;  // at most one wrap (above)
+        if (sj[u] >= jend[u]) {
           sj[u] -= Dw[u];
           ++si[u];
         }
