@@ -148,6 +148,8 @@ struct sift_ctx {
   sift_keypoint* d_kpts = nullptr;
   float* d_desc = nullptr;
   int kp_cap = 0;
+  int* d_perm = nullptr;          // descriptor lane-balance ranking scratch (desc_rank_kernel)
+  int perm_cap = 0;
   int last_n = -1;                // keypoints held from the last host call
   bool last_has_desc = false;
   int* d_err = nullptr;           // sticky error words [assert, workspace, kp capacity] (common.hpp)
@@ -292,6 +294,19 @@ int ensure_kp(sift_ctx* c, int need) {
   HIP_TRY(c, dmalloc(&c->d_kpts, (size_t)need));
   HIP_TRY(c, dmalloc(&c->d_desc, (size_t)need * kDescLen));
   c->kp_cap = need;
+  return SIFT_OK;
+}
+
+// The descriptor's ranking scratch for kp_cap keypoints; grown before any
+// capture (captured sequences name the buffer).
+int ensure_perm(sift_ctx* c, int need) {
+  if (need <= c->perm_cap) return SIFT_OK;
+  drop_graphs(c);
+  if (c->d_perm) (void)hipFree(c->d_perm);
+  c->d_perm = nullptr;
+  c->perm_cap = 0;
+  HIP_TRY(c, dmalloc(&c->d_perm, (size_t)need));
+  c->perm_cap = need;
   return SIFT_OK;
 }
 
@@ -455,8 +470,8 @@ void enqueue_detect(sift_ctx* c, const Layout& L, int batch, sift_keypoint* kpts
 void enqueue_desc(sift_ctx* c, const Layout& L, const sift_keypoint* kpts, const int* img_off,
                   int batch, int kp_cap, float* desc, int first_octave, bool detected) {
   StageScope s(c, ST_DESC);
-  launch_descriptors(c->stream, L, c->d_grad, c->d_mc, kpts, img_off, batch, kp_cap, desc,
-                     first_octave, c->d_err, detected);
+  launch_descriptors(c->stream, L, c->d_grad, c->d_mc, kpts, img_off, batch, std::min(kp_cap, c->perm_cap), desc,
+                     first_octave, c->d_err, detected, c->d_perm);
 }
 
 // End of every compute sequence: status_kernel folds the candidate and
@@ -802,7 +817,7 @@ int sift_ctx_destroy(sift_ctx* c) {
   void* bufs[] = {c->d_stat, c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
                   c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles, c->D.ori_next,
-                  c->d_img_off, c->d_kpts, c->d_desc, c->d_err, c->d_match};
+                  c->d_img_off, c->d_kpts, c->d_desc, c->d_perm, c->d_err, c->d_match};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -900,6 +915,7 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
   const Layout L = make_layout(rows, cols, c->n_oct);
   const Plane src{d_imgs, (long long)row_stride, (long long)img_stride};
   if (int rc = check_fast(c, L, (long long)row_stride)) return rc;
+  if (int rc = ensure_perm(c, kp_cap)) return rc;
   if (c->flags & SIFT_FLAG_VERBOSE) {
     hipEvent_t v0 = get_event(c), v1 = get_event(c), v2 = get_event(c), v3 = get_event(c);
     (void)hipEventRecord(v0, c->stream);
@@ -1151,6 +1167,7 @@ int sift_calc_descriptors(sift_ctx* c, const float* gpyr, int rows, int cols, in
                             c->stream));
   // keypoints may name any scale 0..4 (CV_Assert at src/sift.cpp:744): gradients of all five
   launch_grad(c->stream, L, c->d_gpyr, c->d_grad, 1, 0, kScales - 1, c->d_mc);
+  if ((rc = ensure_perm(c, c->kp_cap))) return rc;
   enqueue_desc(c, L, c->d_kpts, c->d_img_off, 1, c->kp_cap, c->d_desc, first_octave, false);
   enqueue_status(c, false, nullptr, 1, c->kp_cap);  // no detection ran: assertion bit only
   HIP_TRY(c, hipGetLastError());

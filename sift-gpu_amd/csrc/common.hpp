@@ -335,7 +335,8 @@ void launch_status(hipStream_t st, const int* cand_total, int cand_cap, const in
 void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, const MathConsts* mc,
                         const sift_keypoint* kpts, const int* img_kp_off, int batch,
                         int kp_cap, float* desc, int first_octave, int* err_flag,
-                        bool detected);  // detected: keypoints from this library's detection (radius <= 40)
+                        bool detected,  // detected: keypoints from this library's detection (radius <= 40)
+                        int* perm);     // [kp_cap] scratch: the lane-balance ranking
 void launch_math_selftest(hipStream_t st, int op, const float* a, const float* b, float* out, int n,
                           const MathConsts* mc);
 
