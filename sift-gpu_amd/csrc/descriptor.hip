@@ -46,9 +46,13 @@ __device__ __forceinline__ void wave_sync_d() {
 }
 
 constexpr int kGrp = 8;            // keypoints per wave
-constexpr int kRankChunk = 256;    // keypoints ranked together by window size (desc_rank_kernel)
+#ifndef SIFT_DESC_RANK_CHUNK
+#define SIFT_DESC_RANK_CHUNK 256  // A/B builds (tools/build_var.sh): 128, 256, 512
+#endif
+constexpr int kRankChunk = SIFT_DESC_RANK_CHUNK;  // keypoints ranked together by window size (desc_rank_kernel)
 constexpr int kSubPerChunk = kRankChunk / kGrp;
-static_assert(kSubPerChunk == 32, "the sub-batch position hash yields 5 bits");
+constexpr int kSubBits = kSubPerChunk == 16 ? 4 : kSubPerChunk == 32 ? 5 : 6;
+static_assert(kSubPerChunk == 1 << kSubBits, "the sub-batch position hash yields kSubBits bits");
 constexpr int kQBins = 21;         // bins per parity class: 2 x 2 x 5 interior + 1 trash
 constexpr int kTrash = 20;         // qidx of the discarded border bins
 constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
@@ -165,7 +169,7 @@ descriptor_kernel(DescArgs A) {
   for (int sb = slot; sb < nsb; sb += nslot) {
     {
       const int ch = sb / kSubPerChunk;
-      const int pos = (sb % kSubPerChunk) ^ (int)(((unsigned)ch * 0x9E3779B1u) >> 27);
+      const int pos = (sb % kSubPerChunk) ^ (int)(((unsigned)ch * 0x9E3779B1u) >> (32 - kSubBits));
       const int i = k0 + ch * kRankChunk + pos * kGrp + lane;
       if (lane < kGrp) sord[lane] = i < kend ? A.perm[i] : kend;
       wave_sync_d();
