@@ -297,8 +297,8 @@ int ensure_kp(sift_ctx* c, int need) {
   return SIFT_OK;
 }
 
-// The descriptor's ranking scratch for kp_cap keypoints; grown before any
-// capture (captured sequences name the buffer).
+// The descriptor's ranking scratch (one int per keypoint the descriptor pass
+// can see); grown before any capture (captured sequences name the buffer).
 int ensure_perm(sift_ctx* c, int need) {
   if (need <= c->perm_cap) return SIFT_OK;
   drop_graphs(c);
@@ -915,7 +915,9 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
   const Layout L = make_layout(rows, cols, c->n_oct);
   const Plane src{d_imgs, (long long)row_stride, (long long)img_stride};
   if (int rc = check_fast(c, L, (long long)row_stride)) return rc;
-  if (int rc = ensure_perm(c, kp_cap)) return rc;
+  // detection yields at most kMaxPeaks keypoints per candidate slot, so the
+  // ranking scratch never needs more than that, whatever kp_cap the caller gives
+  if (int rc = ensure_perm(c, (int)std::min<long long>(kp_cap, (long long)kMaxPeaks * c->D.cand_cap))) return rc;
   if (c->flags & SIFT_FLAG_VERBOSE) {
     hipEvent_t v0 = get_event(c), v1 = get_event(c), v2 = get_event(c), v3 = get_event(c);
     (void)hipEventRecord(v0, c->stream);

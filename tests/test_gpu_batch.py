@@ -194,6 +194,30 @@ def test_batch_keypoint_capacity(siftgpu, oracle):
         ctx.sync()  # reported once
 
 
+def test_batch_kp_cap_larger_than_the_buffers_need(siftgpu, oracle):
+    """kp_cap is the caller's promise, not an allocation hint: a 2^30 capacity
+    over buffers sized for the real keypoints works (the descriptor's ranking
+    scratch is bounded by the candidate capacity, not by kp_cap)."""
+    import torch
+    B, r, c = 2, 240, 320
+    with siftgpu.Context(r, c, B, device=0) as ctx:
+        imgs = torch.empty((B, r, c), dtype=torch.float32, device="cuda")
+        ctx.synth_images(imgs.data_ptr(), B, r, c, c, r * c, seed_base=60)
+        ref = [oracle.sift(oracle.synth_image(60 + b, r, c)) for b in range(B)]
+        n = sum(len(k) for k, _ in ref)
+        kpts = torch.empty((n, 7), dtype=torch.int32, device="cuda")
+        desc = torch.empty((n, 128), dtype=torch.float32, device="cuda")
+        offs = torch.empty((B + 1,), dtype=torch.int32, device="cuda")
+        ctx.detect_compute_batch(imgs.data_ptr(), B, r, c, c, r * c, kpts.data_ptr(), desc.data_ptr(), 1 << 30,
+                                 offs.data_ptr())
+        ctx.sync()
+        o = offs.cpu().numpy()
+        assert o[B] == n
+        kb = np.concatenate([kp_bytes(k) for k, _ in ref])
+        assert_bits_equal(kpts.cpu().numpy().view(np.uint8).reshape(n, 28), kb, "keypoints")
+        assert_bits_equal(desc.cpu().numpy(), np.concatenate([d for _, d in ref]), "descriptors")
+
+
 def test_graph_cache_rotating_buffers(siftgpu, oracle):
     """a caller rotating among more output buffers than the graph
     cache holds (6 slots, 4 entries) with one shape.  Each new buffer set
