@@ -185,16 +185,16 @@ __host__ __device__ constexpr float ptap(int k) {
 
 // Consumer roles: scales (W2 = 0 for one), accumulator slots P (the smallest
 // multiple of kPB >= 2w + 1; role 2's two scales share the larger cycle), NC
-// = P / kPB steps per slot cycle, planes, h buffers.
+// = P / kPB steps per slot cycle, planes.
 template <int C> struct PcRole;
 template <> struct PcRole<0> {
-  static constexpr int W1 = 18, W2 = 0, P1 = 40, P2 = 1, NC = 5, pl1 = 4, pl2 = 0, h1 = 0, h2 = 0;
+  static constexpr int W1 = 18, W2 = 0, P1 = 40, P2 = 1, NC = 5, pl1 = 4, pl2 = 0;
 };
 template <> struct PcRole<1> {
-  static constexpr int W1 = 12, W2 = 0, P1 = 32, P2 = 1, NC = 4, pl1 = 3, pl2 = 0, h1 = 1, h2 = 1;
+  static constexpr int W1 = 12, W2 = 0, P1 = 32, P2 = 1, NC = 4, pl1 = 3, pl2 = 0;
 };
 template <> struct PcRole<2> {
-  static constexpr int W1 = 8, W2 = 4, P1 = 24, P2 = 12, NC = 3, pl1 = 2, pl2 = 1, h1 = 2, h2 = 3;
+  static constexpr int W1 = 8, W2 = 4, P1 = 24, P2 = 12, NC = 3, pl1 = 2, pl2 = 1;
 };
 static_assert(PcRole<2>::pl1 == kLayers, "the decimated plane (nOctaveLayers) is role 2's first scale");
 
