@@ -1401,7 +1401,10 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
 // reference's raster order (src/sift.cpp:429-437); an invalid sample adds +0.0
 // to bin 0 (exact no-op: every bin is >= +0).
 template <int kOSlots>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2 ? 6 : 1))) void orient_slots_kernel(
+#ifndef SIFT_ORIENT_WPE
+#define SIFT_ORIENT_WPE 6  // A/B builds only (tools/build_var.sh): waves per SIMD orient_slots_kernel<2> is budgeted for
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2 ? SIFT_ORIENT_WPE : 1))) void orient_slots_kernel(
     RefArgs A) {
   constexpr int SB = kOGrp * kOSlots;   // candidates per sub-batch
   constexpr int NSB = 64 / SB;          // sub-batches per ranked chunk
