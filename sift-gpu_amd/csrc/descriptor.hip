@@ -527,8 +527,18 @@ descriptor_kernel(DescArgs A) {
     int odd_cur = 0;
     uint2 qq_cur = make_uint2(0u, 0u);  // PACKED: this owner's 8 bin bytes of the batch
     Loc loc_nxt, loc_alt;  // PF = 2: batches k + 1 and k + 2, located and gathering (two buffers)
+    Loc loc_3rd;           // PF = 3: the third buffer
     if (nmax > 0) {
-      if constexpr (PF == 2) {
+      if constexpr (PF == 3) {
+        Loc l0;
+        locate(0 < nsq, l0);
+        advance();
+        locate(8 < nsq, loc_nxt);
+        advance();
+        locate(16 < nsq, loc_alt);
+        advance();
+        finish(l0, rc_cur, odd_cur);
+      } else if constexpr (PF == 2) {
         Loc l0;
         locate(0 < nsq, l0);
         advance();
@@ -592,8 +602,8 @@ descriptor_kernel(DescArgs A) {
       wave_sync_d();
       RecT<PACKED> rc_nxt;
       int odd_nxt = 0;
-      if constexpr (PF == 2) {
-        locate(base + 16 < nsq, l2);  // batch k + 2: its gather flies for two steps
+      if constexpr (PF >= 2) {
+        locate(base + 8 * PF < nsq, l2);  // batch k + PF: its gather flies for PF steps
         advance();
         finish(ln, rc_nxt, odd_nxt);
       } else {
@@ -636,7 +646,16 @@ descriptor_kernel(DescArgs A) {
       rc_cur = rc_nxt;
       odd_cur = odd_nxt;
     };
-    if constexpr (PF == 2) {
+    if constexpr (PF == 3) {
+      // unrolled by three: the three Loc buffers rotate roles
+      for (int base = 0; base < nmax; base += 24) {
+        step(base, loc_nxt, loc_3rd);
+        if (base + 8 >= nmax) break;
+        step(base + 8, loc_alt, loc_nxt);
+        if (base + 16 >= nmax) break;
+        step(base + 16, loc_3rd, loc_alt);
+      }
+    } else if constexpr (PF == 2) {
       // unrolled by two so the two Loc buffers swap roles instead of being
       // copied (a copy of the gathered pixel would wait for its load)
       for (int base = 0; base < nmax; base += 16) {
@@ -814,8 +833,13 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                      dim3(64), 0, st, A)
   if (packed && detected && deep && one_image_variants(L, batch))
     SIFT_DESC_LAUNCH(true, true, 2, 2);
+#ifdef SIFT_DESC_PF3
+  else if (packed && detected && deep)
+    SIFT_DESC_LAUNCH(true, true, 3, kDescWpe);  // A/B build: gathers three batches ahead
+#else
   else if (packed && detected && deep)
     SIFT_DESC_LAUNCH(true, true, 2, kDescWpe);
+#endif
   else if (packed && detected)
     SIFT_DESC_LAUNCH(true, true, 1, kDescWpe);
   else if (packed)
