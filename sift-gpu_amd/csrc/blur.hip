@@ -733,7 +733,10 @@ void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitc
   A.strips = (cols + 63) / 64;
   A.batch = batch;
   const int w[1] = {kSymW0};
-  sym_plan(A, w, 1, 0.35);  // measured: 4 chunks of a 1080p base, not 2
+#ifndef SIFT_SYM_BASE_CP
+#define SIFT_SYM_BASE_CP 0.35  // A/B builds only (tools/build_var.sh)
+#endif
+  sym_plan(A, w, 1, SIFT_SYM_BASE_CP);  // measured: 4 chunks of a 1080p base, not 2
   hipLaunchKernelGGL(blur_sym_base_kernel, dim3(A.start[1]), dim3(64), 0, st, A);
 }
 
