@@ -736,7 +736,7 @@ descriptor_kernel(DescArgs A) {
 __global__ __launch_bounds__(kRankChunk) void desc_rank_kernel(const sift_keypoint* __restrict__ kpts,
                                                                const int* __restrict__ img_kp_off, int batch,
                                                                int kp_cap, int* __restrict__ perm) {
-  __shared__ int keys[kRankChunk];
+  __shared__ __attribute__((aligned(16))) int keys[kRankChunk];
   int n = img_kp_off[batch];
   if (n > kp_cap) n = kp_cap;
   const int t = threadIdx.x;
@@ -756,10 +756,15 @@ __global__ __launch_bounds__(kRankChunk) void desc_rank_kernel(const sift_keypoi
     __syncthreads();
     keys[t] = key;
     __syncthreads();
+    // four keys per (broadcast) LDS read, unrolled so the reads pipeline
     int rank = 0;
-    for (int u = 0; u < kRankChunk; ++u) {
-      const int ku = keys[u];
-      rank += ku < key || (ku == key && u < t) ? 1 : 0;
+#pragma unroll 8
+    for (int u = 0; u < kRankChunk; u += 4) {
+      const int4 k4 = *reinterpret_cast<const int4*>(&keys[u]);
+      rank += k4.x < key || (k4.x == key && u < t) ? 1 : 0;
+      rank += k4.y < key || (k4.y == key && u + 1 < t) ? 1 : 0;
+      rank += k4.z < key || (k4.z == key && u + 2 < t) ? 1 : 0;
+      rank += k4.w < key || (k4.w == key && u + 3 < t) ? 1 : 0;
     }
     if (i < n) perm[c0 + rank] = i;
   }
