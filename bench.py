@@ -722,6 +722,7 @@ def exact_block(a, world, B, R, C, S, res, tr):
                  if k in stats)
     pyr_bytes = 24.0 * sum(sum((R >> o) * (C >> o) for o in range(a.octaves)) for _ in range(B)) * a.steps
     gathering = res.get("gather") is not None
+    backend = (res.get("gather") or {}).get("backend")
     out.update({
         # first after the metric: the driver's record keeps only the line's head
         "output_verified": bool(verified) and not failed,
@@ -742,7 +743,8 @@ def exact_block(a, world, B, R, C, S, res, tr):
                    "global_batch": world * B, "rows": R, "cols": C, "octaves": a.octaves,
                    "mode": "exact (bit-identical to the CPU path)",
                    "parallelism": f"image-sharded x{world}, {S} HIP streams x {B // S} images per GPU" +
-                                  (", RCCL keypoint gather one step behind" if gathering else "")},
+                                  (f", keypoint gather to rank 0 one step behind over {gather_label(backend)}"
+                                   if gathering else "")},
         "keypoints_per_s": round(kp_total_step * a.steps / dt, 1),
         "keypoints_per_step": int(kp_total_step),
         "roofline": roof,
@@ -769,6 +771,15 @@ def exact_block(a, world, B, R, C, S, res, tr):
                                                              (d["ms"] * 1e-3), 1),
                              "roofline": descriptor_roofline(tr, d)}
     return out
+
+
+def gather_label(backend) -> str:
+    """What actually carried the keypoint gather: torch.distributed's "nccl"
+    backend is RCCL on ROCm; anything else (the shared-GPU gloo rehearsal)
+    is named as what it is."""
+    if backend == "nccl":
+        return "RCCL (torch.distributed nccl backend, xGMI p2p)"
+    return f"{backend} (host-staged; not RCCL)"
 
 
 def fast_kernel():
@@ -819,7 +830,7 @@ def match_block(a, world, match):
                      "note": "2 VALU lane-ops (v_sub, v_add |x|) per descriptor element per pair; "
                              "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"},
         "note": "SURVEY 8(f) f2 (src/main.cpp:25-27); bit-exact vs oracle/match.py"}
-    if world == 1 and not a.no_cpu_baseline:
+    if not a.no_cpu_baseline:
         m["cpu_baseline"] = match_cpu_baseline(match)
     return m
 
@@ -870,18 +881,59 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+CPU_JSON_ENV = "SIFT_BENCH_CPU_JSON"
+
+
+def wants_cpu_legs(a) -> bool:
+    return not a.no_cpu_baseline and a.only is None
+
+
+def save_cpu_legs(cpu, errors, path):
+    with open(path, "w") as f:
+        json.dump({"cpu": cpu, "errors": errors}, f)
+
+
+def load_cpu_legs(path, errors):
+    """Rank 0 of an N > 1 run: the CPU legs its launching parent measured
+    (launch_ranks) -- merged into the line exactly as at N = 1."""
+    with open(path) as f:
+        d = json.load(f)
+    errors.update(d.get("errors") or {})
+    return d.get("cpu") or None
+
+
 def launch_ranks(a, argv=None) -> int:
     """`--gpus N > 1` without a launcher: run N ranks of this script under
     torch.distributed.run as a CHILD process (never an exec: nothing here has
     touched the GPU, and the child's ranks initialise their own devices), one
-    rank per GPU, rendezvous on 127.0.0.1.  Rank 0's line reaches our stdout
-    through the inherited descriptor; returns the child's exit code."""
+    rank per GPU, rendezvous on 127.0.0.1.  The CPU baselines (SURVEY 8(d) d4:
+    the reference path on the node's own cores, in the same run at every GPU
+    count) are measured here first, while no process of the run holds a GPU,
+    and reach rank 0 as a JSON file named by SIFT_BENCH_CPU_JSON.  Rank 0's
+    line reaches our stdout through the inherited descriptor; returns the
+    child's exit code."""
     argv = sys.argv[1:] if argv is None else argv
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    tmp = None
+    if wants_cpu_legs(a):
+        import tempfile
+        errors = {}
+        cpu = cpu_legs(a, errors)
+        fd, tmp = tempfile.mkstemp(prefix="sift_bench_cpu_", suffix=".json")
+        os.close(fd)
+        save_cpu_legs(cpu, errors, tmp)
+        env[CPU_JSON_ENV] = tmp
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
     print(f"bench.py: launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
-    return subprocess.run(cmd, env=env).returncode
+    try:
+        return subprocess.run(cmd, env=env).returncode
+    finally:
+        if tmp is not None:
+            try:
+                os.unlink(tmp)
+            except OSError:
+                pass
 
 
 def rehearsal():
@@ -930,10 +982,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     errors = {}
     cpu = None
-    if world == 1 and not a.no_cpu_baseline and a.only is None:
-        # before this process touches the GPU: the image-parallel leg starts
-        # child processes
-        cpu = cpu_legs(a, errors)
+    if rank == 0 and wants_cpu_legs(a):
+        if world > 1 and os.environ.get(CPU_JSON_ENV):
+            # measured by launch_ranks before any rank started
+            cpu = guarded(errors, "cpu_legs", load_cpu_legs, os.environ[CPU_JSON_ENV], errors)
+        else:
+            # N = 1, or ranks started by an outside launcher: rank 0 measures
+            # them before this process touches the GPU (the image-parallel leg
+            # starts child processes); the other ranks wait at the rendezvous
+            cpu = cpu_legs(a, errors)
     if world > 1:
         dev = local % torch.cuda.device_count() if rehearsal() else local
         torch.cuda.set_device(dev)

@@ -1090,7 +1090,13 @@ int sift_build_gaussian_pyramid(sift_ctx* c, const float* img, int rows, int col
   if ((rc = check_fast(c, L, c->in_pitch))) return rc;
   if ((rc = upload_image(c, img, rows, cols, (size_t)cols * sizeof(float)))) return rc;
   enqueue_pyramid(c, L, Plane{c->d_in, c->in_pitch, c->in_img}, 1, false);
+  // SIFT_FLAG_FAST: an expired in-kernel wait of pyr_pc_kernel (err[3]) means
+  // the planes are invalid -- reported by this call, and consumed so that it
+  // cannot surface in a later one
+  enqueue_status(c, false, nullptr, 1, c->kp_cap);
   HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if ((rc = take_status(c, false, kErrStall))) return rc;
   if ((rc = copy_pyramid(c, L, c->d_gpyr, nullptr, gpyr, kScales))) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return SIFT_OK;

@@ -219,3 +219,61 @@ def test_line_survives_failing_block(bench, monkeypatch, capsys):
         monkeypatch.setattr(bench, leg, lambda *a, **k: None)
     out = _run(bench, monkeypatch, capsys, ["--no-cpu-baseline"])
     assert out["value"] > 0 and "error" in out["fast_mode"]
+
+
+def test_launcher_cpu_legs_reach_rank0_line(bench, monkeypatch, capsys, tmp_path):
+    """at N > 1 the launching parent measures the CPU legs
+    before any rank exists and rank 0 merges them; the gather is labelled by
+    the backend that carried it (a gloo rehearsal never claims RCCL)."""
+    import torch
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    seen = {}
+    fake_env = bench.Env
+
+    def fake_run(cmd, env=None, **k):
+        seen["path"] = env[bench.CPU_JSON_ENV]
+        with open(seen["path"]) as f:
+            seen["payload"] = json.load(f)
+        return subprocess.CompletedProcess(cmd, 0)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(bench, "Env", lambda *a, **k: pytest.fail("the launcher touched the GPU"))
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 0
+    assert seen["payload"]["cpu"]["cpu_baseline"]["value"] == 0.6
+    assert not os.path.exists(seen["path"])   # the parent cleans up after the child
+
+    # rank 0 of the child: reads the parent's file, runs no CPU leg itself
+    monkeypatch.setattr(bench, "Env", fake_env)
+    cpu_file = tmp_path / "cpu.json"
+    bench.save_cpu_legs(seen["payload"]["cpu"], {"cpu_baseline_gpu_share": "canned failure"}, str(cpu_file))
+    monkeypatch.setattr(bench, "cpu_baseline", lambda *a, **k: pytest.fail("rank 0 re-ran the CPU leg"))
+    _quiet_legs(bench, monkeypatch)
+    gather = {"backend": "gloo", "world_size": 2}
+    monkeypatch.setattr(bench, "run_exact", lambda env: {"exact": (0.1, {}, 800000.0),
+                                                         "prof": (0.12, _stats(), 0.0),
+                                                         "verified": [0, 31, 63], "failed": [],
+                                                         "gather": gather})
+    monkeypatch.setattr(bench.dist, "init_process_group", lambda *a, **k: None)
+    monkeypatch.setattr(bench.dist, "destroy_process_group", lambda *a, **k: None)
+    monkeypatch.setattr(bench.dist, "get_backend", lambda *a, **k: "gloo")
+    for k, v in (("WORLD_SIZE", "2"), ("RANK", "0"), ("LOCAL_RANK", "0"), (bench.CPU_JSON_ENV, str(cpu_file)),
+                 ("SIFT_BENCH_SHARE_GPU", "1"), ("SIFT_BENCH_DIST_BACKEND", "gloo")):
+        monkeypatch.setenv(k, v)
+    out = _run(bench, monkeypatch, capsys, ["--gpus", "2"])
+    assert out["n_gpus"] == 2 and out["cpu_baseline"]["value"] == 0.6
+    assert out["speedup_vs_cpu_1thread"]["Mpix/s"] > 0
+    assert out["leg_errors"]["cpu_baseline_gpu_share"] == "canned failure"
+    par = out["config"]["parallelism"]
+    assert "gloo" in par and "not RCCL" in par and out["distributed"]["backend"] == "gloo"
+
+    # the same rank under an outside launcher (no parent file): rank 0 measures
+    monkeypatch.delenv(bench.CPU_JSON_ENV)
+    monkeypatch.setattr(bench, "cpu_baseline", lambda r, c, threads=1, min_seconds=0.0: {
+        "value": 0.7, "unit": "Mpix/s", "cores": threads, "kind": "port", "keypoints_per_s": 4100.0,
+        "sample": "canned"})
+    gather["backend"] = "nccl"
+    out = _run(bench, monkeypatch, capsys, ["--gpus", "2"])
+    assert out["cpu_baseline"]["value"] == 0.7 and "RCCL" in out["config"]["parallelism"]
