@@ -287,7 +287,7 @@ void so_build_gaussian_pyramid(const float* img, int rows, int cols, int n_octav
 
 /* ---- SIFT_FLAG_FAST pyramid (the library's separable form) -------------
  * Not the reference's arithmetic: the separable agreement mode of
- * sift-gpu_amd/csrc/pyramid_tri.hip, restated here so that its planes can be
+ * sift-gpu_amd/csrc/pyramid_pc.hip, restated here so that its planes can be
  * checked bit for bit.  Taps g(a) = (float)(exp(-a^2 / den) / sqrt(2 pi s^2))
  * with den = (double)(2 s s) in float (the square root of getGaussianKernel's
  * normalisation, src/sift.cpp:97-107).  Every blur reads its source with zero

@@ -128,9 +128,9 @@ struct sift_ctx {
   float* d_coef = nullptr;        // base (w=4) then the 4 octave scales
   float* d_coef_gen = nullptr;    // per-call coefficients (Gaussian_Blur / _1D)
   bool fast_ok = false;           // SIFT_FLAG_FAST: pyramid_pc.hip's compiled-in taps equal the host's
-  bool fuse_dec = true;           // 2-D tile blurs write the next plane 0 (SIFT_HIP_FUSE_DEC=0: decimate_kernel)
-  bool poison_pad = false;        // test switch SIFT_HIP_POISON_PAD=1: NaN into every plane's pitch padding
-  bool sym_xcd = true;            // scatter blur in XCD-contiguous wave order (SIFT_HIP_SYM_XCD=0: launch order, A/B)
+  // test hooks (SIFT_HIP_TEST_HOOKS, a comma list read at context creation; tests only):
+  bool poison_pad = false;        // "poison_pad": NaN into every plane's pitch padding after the pyramid
+  bool stall_once = false;        // "pc_stall_once": the next pyr_pc_kernel launch gets an expired wait bound
   // exact blur: launches with fewer 8-pixel tile workgroups than this use the
   // 2-output-per-lane tiles (blur_small_kernel); SIFT_HIP_SMALL_MAX overrides
   long long small_max = 2048;
@@ -393,7 +393,8 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
         launch_decimate(st, L, o, c->d_gpyr, batch);
       }
       StageScope s(c, ST_PYR_FAST, 2.0 * taps * px, 24.0 * px);
-      launch_pyramid_pc(st, L, o, c->d_gpyr, src, batch, c->d_err + 3);
+      launch_pyramid_pc(st, L, o, c->d_gpyr, src, batch, c->d_err + 3, c->stall_once);
+      c->stall_once = false;
     }
     if (c->poison_pad) enqueue_poison_pad(c, L, batch);
     if (with_dog)
@@ -408,8 +409,7 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
     const int k = 2 * c->w_base + 1;
     StageScope s(c, ST_BLUR_BASE, 2.0 * k * k * px, 8.0 * px);
     if (use_sym_blur(c, L.oct[0].rows, L.oct[0].cols, batch))
-      launch_blur_base_sym(st, src, c->d_gpyr + L.oct[0].g_off[0], L.oct[0].pitch, L.g_img, L.rows, L.cols, batch,
-                           c->sym_xcd);
+      launch_blur_base_sym(st, src, c->d_gpyr + L.oct[0].g_off[0], L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
     else
       launch_blur_plane(st, c->w_base, c->d_coef + c->coef_base_off, src, c->d_gpyr + L.oct[0].g_off[0],
                         L.oct[0].pitch, L.g_img, L.rows, L.cols, batch);
@@ -428,10 +428,10 @@ void enqueue_pyramid(sift_ctx* c, const Layout& L, Plane src, int batch, bool wi
       double taps = 0;
       for (int q = 0; q < 4; ++q) taps += (double)(2 * c->wsz[q] + 1) * (2 * c->wsz[q] + 1);
       const bool sym = use_sym_blur(c, L.oct[o].rows, L.oct[o].cols, batch);
-      const bool fuse = c->fuse_dec && o + 1 < L.n_oct && blur_fuses_decimation(L, o + 1);
+      const bool fuse = o + 1 < L.n_oct && blur_fuses_decimation(L, o + 1);
       StageScope s(c, sym ? ST_BLUR_SYM : ST_BLUR_OCT, 2.0 * taps * px, 20.0 * px);
       if (sym)
-        launch_blur_octave_sym(st, L, o, c->d_gpyr, batch, fuse, c->sym_xcd);
+        launch_blur_octave_sym(st, L, o, c->d_gpyr, batch, fuse);
       else if (blur_octave_tiles(L, o, batch) < c->small_max)
         launch_blur_octave_small(st, L, o, c->d_gpyr, c->d_coef + c->coef_oct_off, c->wsz, batch, fuse);
       else
@@ -765,14 +765,10 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   // mismatch with the host formula makes the flag an error (enqueue-time check)
   c->fast_ok = fast_taps_match(sb, sig_f);
   {
-    const char* fd = getenv("SIFT_HIP_FUSE_DEC");
-    c->fuse_dec = !(fd && atoi(fd) == 0);
-    const char* pp = getenv("SIFT_HIP_POISON_PAD");
-    c->poison_pad = pp && atoi(pp) != 0;
-    const char* sx = getenv("SIFT_HIP_SYM_XCD");
-    // XCD-contiguous order by default (round 5): -36 % blur read traffic,
-    // headline equal or +0.1 % (profiles/r5_blur_xcd_ab.txt)
-    c->sym_xcd = !(sx && atoi(sx) == 0);
+    const char* th = getenv("SIFT_HIP_TEST_HOOKS");
+    const std::string hooks = "," + std::string(th ? th : "") + ",";
+    c->poison_pad = hooks.find(",poison_pad,") != std::string::npos;
+    c->stall_once = hooks.find(",pc_stall_once,") != std::string::npos;
   }
   MathConsts mc;
   host_math_consts(&mc);
@@ -793,7 +789,7 @@ int sift_ctx_create(int device, int max_rows, int max_cols, int max_batch, unsig
   c->blk_cap = mask_blocks_per_image(L) * max_batch;
   if (dmalloc(&c->D.mask, (size_t)mask_words_per_image(L) * max_batch) != hipSuccess ||
       dmalloc(&c->D.blk_counts, c->blk_cap) != hipSuccess ||
-      dmalloc(&c->D.cand_total, 1) != hipSuccess || dmalloc(&c->D.ori_next, 8) != hipSuccess ||
+      dmalloc(&c->D.cand_total, 1) != hipSuccess ||
       dmalloc(&c->D.img_cand_off, max_batch + 1) != hipSuccess ||
       dmalloc(&c->D.kp_total, 1) != hipSuccess || dmalloc(&c->d_img_off, max_batch + 1) != hipSuccess ||
       alloc_candidates(c, (int)cap) != SIFT_OK)
@@ -816,7 +812,7 @@ int sift_ctx_destroy(sift_ctx* c) {
   if (c->h_stat) (void)hipHostFree(c->h_stat);
   void* bufs[] = {c->d_stat, c->d_in, c->d_gpyr, c->d_dog, c->d_tmp, c->d_grad, c->d_coef, c->d_coef_gen, c->d_mc,
                   c->D.mask, c->D.blk_counts, c->D.cand_total, c->D.img_cand_off, c->D.cands, c->D.couts,
-                  c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles, c->D.ori_next,
+                  c->D.kp_scan, c->D.kp_total, c->D.npeaks, c->D.scan_tmp, c->D.scan_tiles,
                   c->d_img_off, c->d_kpts, c->d_desc, c->d_perm, c->d_err, c->d_match};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -945,6 +941,7 @@ int enqueue_ncl(sift_ctx* c, const float* d_imgs, int batch, int rows, int cols,
   key_put(key, kp_cap);
   key_put(key, c->n_oct);
   key_put(key, c->flags);
+  key_put(key, c->stall_once);  // test hook: a captured poll bound must not be replayed
   key_put(ptrs, d_imgs);
   key_put(ptrs, d_kpts);
   key_put(ptrs, d_desc);

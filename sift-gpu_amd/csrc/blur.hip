@@ -500,22 +500,18 @@ struct SymArgs {
   int rows, cols, strips, batch;
   int start[5];        // first wave of each slot; start[nslot] = grid size
   int chunk[4];        // output rows per wave, per slot
-  int count[4];        // waves of each slot (xcd: start[] spaced by count rounded up to 8)
-  int xcd;             // XCD-contiguous order (SIFT_HIP_SYM_XCD=1, A/B): blocks b, b + 8, ... take consecutive waves
+  int count[4];        // waves of each slot (start[] spaced by count rounded up to 8: whole XCD runs)
 };
 
-// Wave index within slot `slot` of block `wid`; -1: a padding block.  With
-// A.xcd the blocks of one XCD (b, b + 8, ... under round-robin placement,
-// speed only) take a contiguous run of the slot's waves, so neighbouring
-// strips -- which read each other's w halo columns -- meet in one L2.
+// Wave index within slot `slot` of block `wid`; -1: a padding block.  The
+// blocks of one XCD (b, b + 8, ... under round-robin placement, speed only)
+// take a contiguous run of the slot's waves, so neighbouring strips -- which
+// read each other's w halo columns -- meet in one L2 (round 5: -36 % read
+// traffic, same time -- the kernel is VALU-bound; profiles/r5_blur_xcd_ab.txt).
 __device__ __forceinline__ int sym_local(const SymArgs& A, int slot, int wid) {
-  int local = wid - A.start[slot];
-  if (A.xcd) {
-    const int n8 = A.start[slot + 1] - A.start[slot];
-    local = (local & 7) * (n8 >> 3) + (local >> 3);
-    if (local >= A.count[slot]) return -1;
-  }
-  return local;
+  const int n8 = A.start[slot + 1] - A.start[slot];
+  const int local = ((wid - A.start[slot]) & 7) * (n8 >> 3) + ((wid - A.start[slot]) >> 3);
+  return local < A.count[slot] ? local : -1;
 }
 
 // Wave-scope ordering of LDS accesses across lanes: no instruction, but the
@@ -713,15 +709,14 @@ static void sym_plan(SymArgs& A, const int* w, int nslot, double cp) {
     A.chunk[s] = h;
     A.start[s] = start;
     A.count[s] = A.strips * A.batch * ch;
-    start += A.xcd ? (A.count[s] + 7) / 8 * 8 : A.count[s];
+    start += (A.count[s] + 7) / 8 * 8;
   }
   for (int s = nslot; s < 5; ++s) A.start[s] = start;
 }
 
 void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitch, long long dimg, int rows,
-                          int cols, int batch, bool xcd) {
+                          int cols, int batch) {
   SymArgs A{};
-  A.xcd = xcd;
   A.src = src.p;
   A.s_pitch = src.pitch;
   A.s_img = src.img_stride;
@@ -740,11 +735,9 @@ void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitc
   hipLaunchKernelGGL(blur_sym_base_kernel, dim3(A.start[1]), dim3(64), 0, st, A);
 }
 
-void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next,
-                            bool xcd) {
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next) {
   const Octave& O = L.oct[o];
   SymArgs A{};
-  A.xcd = xcd;
   const NextPlane nx = next_plane(L, o, gpyr, fuse_next);
   A.nxt = nx.p;
   A.n_pitch = nx.pitch;

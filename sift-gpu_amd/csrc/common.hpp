@@ -42,7 +42,7 @@ constexpr double kCvPi = 3.1415926535897932384626433832795;
 // (pyramid_pc.hip) write whole 4-column groups past cols there, and no kernel
 // reads a column >= cols of a Gaussian or DoG plane (every reader bounds its
 // columns by cols, and the sub-module API copies planes out row by row with
-// cols columns); tests/test_gpu_fast.py::test_fast_ignores_pitch_padding
+// cols columns); tests/test_gpu_fast.py::test_pitch_padding_is_never_read
 // poisons the padding with NaN and requires unchanged results.
 constexpr int kPitchAlign = 32;
 struct Octave {
@@ -250,9 +250,8 @@ long long blur_octave_tiles(const Layout& L, int o, int batch);
 // context's base + octave tables before these are used.
 bool sym_tables_match(const float* coefs);
 void launch_blur_base_sym(hipStream_t st, Plane src, float* dst, long long dpitch, long long dimg, int rows,
-                          int cols, int batch, bool xcd);
-void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next,
-                            bool xcd);
+                          int cols, int batch);
+void launch_blur_octave_sym(hipStream_t st, const Layout& L, int o, float* gpyr, int batch, bool fuse_next);
 void launch_decimate(hipStream_t st, const Layout& L, int o, float* gpyr, int batch);
 void launch_dog(hipStream_t st, const Layout& L, int o, const float* gpyr, float* dog, int batch);
 void launch_blur_1d(hipStream_t st, int w, const float* coef1d, Plane src, float* tmp, float* dst,
@@ -275,7 +274,8 @@ void launch_knn_l1(hipStream_t st, const float* q, int nq, const float* t, int n
 // (kErrStall).  fast_taps_match: the compiled-in 1-D taps equal
 // fast_taps_host's for these sigmas; pyramid_fast_fits: every plane and the
 // input rows below the kernel's dropped-offset range.
-void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch, int* err);
+void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch, int* err,
+                       bool stall_test = false);  // stall_test: the pc_stall_once test hook
 bool pyramid_fuses_decimation(const Layout& L, int o);
 bool fast_taps_match(float sigma_base, const float* sig);
 bool pyramid_fast_fits(const Layout& L, long long src_row_stride);
@@ -309,7 +309,6 @@ struct DetectBufs {
   int* npeaks;          // orientation peaks per candidate, [cand_cap]
   int* scan_tmp;        // exclusive scan of blk_counts, [blk_cap+1]
   int* scan_tiles;      // per-tile sums of the multi-block scan, [scan_tiles_for(max(blk_cap, cand_cap))]
-  int* ori_next;        // [8] per-XCD candidate counters of the one-image orientation pass (refine_kernel zeroes them)
 };
 int scan_tiles_for(long long cap);
 long long mask_words_per_image(const Layout& L);

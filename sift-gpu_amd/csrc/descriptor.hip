@@ -18,10 +18,9 @@
 //    per-lane LDS read-modify-writes, no atomics, no cross-lane hazards.  The
 //    histogram lives at [qidx][lane] (qidx = (R'>>1)*10 + (C'>>1)*5 + (O>>1)
 //    over the interior rows / columns R' = R-1, C' = C-1 in [0, 4) -- the only
-//    bins the fold reads; a border-bin update goes to a trash row, or, in the
-//    packed form, carries +0.0 into an interior bin), so all 64
-//    lanes of an update hit distinct banks and a wave needs 5.4 KB, not
-//    11.5 KB (three waves per SIMD instead of two).
+//    bins the fold reads; a border-bin update carries +0.0 into an interior
+//    bin), so all 64 lanes of an update hit distinct banks and a wave needs
+//    5.1 KB, not 11.5 KB.
 //  * Fold, 0.2 clamp, uchar quantisation, RootSIFT (src/sift.cpp:676-721)
 //    keep the reference's sequential sums (lane 0 of the group).
 #include "common.hpp"
@@ -53,11 +52,9 @@ constexpr int kRankChunk = SIFT_DESC_RANK_CHUNK;  // keypoints ranked together b
 constexpr int kSubPerChunk = kRankChunk / kGrp;
 constexpr int kSubBits = kSubPerChunk == 16 ? 4 : kSubPerChunk == 32 ? 5 : 6;
 static_assert(kSubPerChunk == 1 << kSubBits, "the sub-batch position hash yields kSubBits bits");
-constexpr int kQBins = 21;         // bins per parity class: 2 x 2 x 5 interior + 1 trash
-constexpr int kTrash = 20;         // qidx of the discarded border bins
+constexpr int kQBins = 20;         // bins per parity class: 2 x 2 x 5 interior
 constexpr int kMaxWinRows = 81;    // window rows with a row table (radius <= 40)
 constexpr int kRowsTab = kMaxWinRows + 2;  // + the entries D, D + 1 the walk reads past its last row (unused values)
-constexpr int kRecStride2 = 132;   // words per sample row of the owner records (128 + pad)
 
 struct DescArgs {
   Layout L;
@@ -94,23 +91,18 @@ __device__ __forceinline__ void slab(float a, float inv_a, float b, int& lo, int
   hi = min(hi, (int)fminf(floorf(x1), 1e6f));
 }
 
-// Record hand-off, two forms (same sums, same bits):
-//   PACKED = false: records (qidx, value) as float2 at [sample][group][owner]
-//     (4.2 KB), a 32-bit row table (2.6 KB): 12.4 KB of LDS per wave;
-//   PACKED = true: values at [group][owner][sample] (2 KB, XOR-swizzled so
-//     the owner's two ds_read_b128 are conflict free and each store address
-//     is one XOR), bin bytes at [group][owner][sample] (0.5 KB, one
-//     ds_read_b64), a 16-bit row table (1.3 KB): 9.4 KB per wave, and the
-//     in-flight records packed as 8 values + 2 words of bin bytes, so four
-//     waves per SIMD fit instead of three.
-constexpr int kRecG = 64;  // PACKED value words per group (8 owners x 8 samples, XOR-swizzled, see the store)
+// Record hand-off (packed, round 2): values at [group][owner][sample] (2 KB,
+// XOR-swizzled so the owner's two ds_read_b128 are conflict free and each
+// store address is one XOR), the bin bytes handed to their owners in
+// registers (round 4), a 16-bit row table for caller keypoints (1.3 KB; DET:
+// 32-bit cumulative entries, 2.7 KB), and the in-flight records packed as 8
+// values + 2 words of bin bytes, so four waves per SIMD fit.  (Round 1's
+// float2 (qidx, value) records at [sample][group][owner] with a trash row,
+// 12.4 KB per wave and three waves per SIMD, were 8.71 vs 8.39 ms per step:
+// tools/patches/r5_variants.patch.)
+constexpr int kRecG = 64;  // value words per group (8 owners x 8 samples, XOR-swizzled, see the store)
 
-template <bool PACKED>
-struct RecT {  // one lane's 8 corner records: (qidx, value) pairs
-  float4 r[4];
-};
-template <>
-struct RecT<true> {
+struct RecT {  // one lane's 8 corner records
   float v[8];
   unsigned qb[2];  // byte s (word s >> 2): qidx of corner s ^ odd, the one owner slot s takes
 };
@@ -124,21 +116,23 @@ struct RecT<true> {
 // whole step -- a wave that is alone on its SIMD (one image) no longer waits a
 // full memory latency per batch, and at four waves per SIMD (batches) the
 // descriptor took 6.36-6.38 vs 6.49-6.54 ms per 64 x 1080p step
-// (profiles/r4_desc_pf2_ab.txt).  WPE: waves per SIMD the registers are
-// budgeted for (PF = 2 at 4: 128 VGPRs, the spills outside the sample loop).
-template <bool PACKED, bool DET, int PF, int WPE>
+// (profiles/r4_desc_pf2_ab.txt; three batches ahead, 38 spills: 5.56-5.58 vs
+// 5.50-5.51, round 5).  WPE: waves per SIMD the registers are budgeted for
+// (PF = 2 at 4: 128 VGPRs, the spills outside the sample loop).
+template <bool DET, int PF, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 descriptor_kernel(DescArgs A) {
-  // [qidx][group*8 + parity]; the packed form has no trash row
-  constexpr int kHistRows = PACKED ? kQBins - 1 : kQBins;
+  static_assert(PF == 1 || PF == 2, "one or two sample batches in flight");
+  // [qidx][group*8 + parity]
+  constexpr int kHistRows = kQBins;
   __shared__ float hist[kHistRows * 64];
   // per-sample hand-off records (see RecT); outside the sample loop the same
   // words hold the sub-batch's keypoint indices and the normalisation scalars
-  __shared__ __attribute__((aligned(16))) float rec[PACKED ? kGrp * kRecG : 8 * kRecStride2];
-  // per row: (jlo + 64) | len << 16 (PACKED: << 8, 16 bits); DET: (jb << 16) | cum
-  // (see the walk below)
-  __shared__ typename std::conditional<PACKED && !DET, unsigned short, int>::type rows_tab[kGrp][kRowsTab];
-  constexpr int kLenSh = PACKED ? 8 : 16, kLoMask = PACKED ? 0xff : 0xffff;
+  __shared__ __attribute__((aligned(16))) float rec[kGrp * kRecG];
+  // per row: (jlo + 64) | len << 8 (16 bits); DET: (jb << 16) | cum (see the
+  // walk below)
+  __shared__ typename std::conditional<!DET, unsigned short, int>::type rows_tab[kGrp][kRowsTab];
+  constexpr int kLenSh = 8, kLoMask = 0xff;
   int* const sord = reinterpret_cast<int*>(rec);                 // [kGrp] keypoint indices
   float(*const bc)[4] = reinterpret_cast<float(*)[4]>(rec + kGrp);  // [kGrp][4] normalisation scalars
   const int lane = threadIdx.x & 63;
@@ -326,11 +320,10 @@ descriptor_kernel(DescArgs A) {
     // their parity bits, corner k = dr*4 + dc*2 + do lands in interior bin
     // (Rm+dr, Cm+dc, O0+do), whose parity -- its owner -- is k ^ odd, at
     //   qidx_k = qi0 + [dr and Rm odd]*10 + [dc and Cm odd]*5 + [do and O0 odd],
-    // or outside the interior when Rm+dr or Cm+dc leaves [0, 4) (trash row;
-    // packed form: value +0.0).
+    // or outside the interior when Rm+dr or Cm+dc leaves [0, 4) (value +0.0).
     // The record (qidx_k, value_k) is stored straight into owner slot k ^ odd;
     // the owner adds its lane to form the [qidx][lane] address.
-    RecT<PACKED> rc_cur;  // (qidx, val) x 8 corners of this lane's sample
+    RecT rc_cur;  // (qidx, val) x 8 corners of this lane's sample
     // locate: the sample at the walk position, its gather (in flight until
     // finish uses it) and the parts of its record that do not need the pixel
     // (weight, spatial bins); finish: the rest.
@@ -377,7 +370,7 @@ descriptor_kernel(DescArgs A) {
       L.X = DET ? min(max(xr, 0), d) : L.ok ? xr : 1;
       L.Y = DET ? min(max(yc, 0), d) : L.ok ? yc : 1;
     };
-    auto finish = [&](const Loc& L, RecT<PACKED>& out, int& odd_out) {
+    auto finish = [&](const Loc& L, RecT& out, int& odd_out) {
       const float rbin = L.rbin, cbin = L.cbin;
       const bool ok = L.ok;
       // An invalid sample must add +0.0 everywhere.  Caller keypoints: its
@@ -408,22 +401,19 @@ descriptor_kernel(DescArgs A) {
       const int X = L.X, Y = L.Y, Rm = X - 1, Cm = Y - 1;  // Rm, Cm: the unpacked form only
       const int odd = ((Rm & 1) << 2) | ((Cm & 1) << 1) | (O0 & 1);
       float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-      if constexpr (PACKED) {
-        // corners outside the interior rows carry +0.0 (added to some interior
-        // bin: an exact no-op, every bin is >= +0) instead of going to a
-        // trash bin; each weight is masked after every product that uses its
-        // unmasked value, so the interior corners' values are unchanged
-        v_r0 = X >= 1 ? v_r0 : 0.f;  // Rm >= 0
-        v_r1 = X <= 3 ? v_r1 : 0.f;  // Rm <= 2
-      }
+      // corners outside the interior rows carry +0.0 (added to some interior
+      // bin: an exact no-op, every bin is >= +0) instead of going to a trash
+      // bin; each weight is masked after every product that uses its
+      // unmasked value, so the interior corners' values are unchanged
+      v_r0 = X >= 1 ? v_r0 : 0.f;  // Rm >= 0
+      v_r1 = X <= 3 ? v_r1 : 0.f;  // Rm <= 2
       float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
       float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-      if constexpr (PACKED) {  // and outside the interior columns
-        v_rc00 = Y >= 1 ? v_rc00 : 0.f;
-        v_rc10 = Y >= 1 ? v_rc10 : 0.f;
-        v_rc01 = Y <= 3 ? v_rc01 : 0.f;
-        v_rc11 = Y <= 3 ? v_rc11 : 0.f;
-      }
+      // and outside the interior columns
+      v_rc00 = Y >= 1 ? v_rc00 : 0.f;
+      v_rc10 = Y >= 1 ? v_rc10 : 0.f;
+      v_rc01 = Y <= 3 ? v_rc01 : 0.f;
+      v_rc11 = Y <= 3 ? v_rc11 : 0.f;
       float v[8];
       v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
       v[6] = v_rc11 - v[7];
@@ -433,7 +423,7 @@ descriptor_kernel(DescArgs A) {
       v[2] = v_rc01 - v[3];
       v[1] = v_rc00 * obin;
       v[0] = v_rc00 - v[1];
-      if constexpr (PACKED) {
+      {
 #pragma unroll
         for (int k = 0; k < 8; ++k) out.v[k] = v[k];
         // bin bytes in owner-slot order: byte s (word s >> 2) is the qidx of
@@ -455,28 +445,14 @@ descriptor_kernel(DescArgs A) {
         const unsigned c4 = __builtin_amdgcn_perm(0x00000505u, 0x05000000u, selC) + o4;
         out.qb[0] = __builtin_amdgcn_perm(0x00000a0au, 0x0a000000u, selR0) + c4;
         out.qb[1] = __builtin_amdgcn_perm(0x00000a0au, 0x0a000000u, selR1) + c4;
-      } else {
-        // corner k's bin index qidx_k (independent of the owner); the store
-        // places it in owner slot k ^ odd, so no value permutation here
-        const int qi0 = __mul24(Rm >> 1, 10) + (Cm >> 1) * 5 + (O0 >> 1);
-        const int a10 = (Rm & 1) ? 10 : 0, a5 = (Cm & 1) ? 5 : 0, a1 = O0 & 1;
-        const bool r0v = Rm >= 0, r1v = Rm <= 2, c0v = Cm >= 0, c1v = Cm <= 2;
-        const int q1 = qi0 + a1, q2 = qi0 + a5, q4 = qi0 + a10;
-        const int qk[8] = {r0v && c0v ? qi0 : kTrash,      r0v && c0v ? q1 : kTrash,
-                           r0v && c1v ? q2 : kTrash,       r0v && c1v ? q2 + a1 : kTrash,
-                           r1v && c0v ? q4 : kTrash,       r1v && c0v ? q4 + a1 : kTrash,
-                           r1v && c1v ? q4 + a5 : kTrash,  r1v && c1v ? q4 + a5 + a1 : kTrash};
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          out.r[t] = make_float4(__int_as_float(qk[2 * t]), v[2 * t], __int_as_float(qk[2 * t + 1]),
-                                 v[2 * t + 1]);
       }
-      // PACKED: the slot bits of the hand-off store address from the parities
-      // of X = Rm + 1 and Y = Cm + 1 -- (odd ^ 6) << 5, i.e. slot s is stored
-      // at position s ^ 6 (the owner reads there) -- by shift-and-or steps
-      odd_out = PACKED ? ((X << 7) & 0x80) | ((Y << 6) & 0x40) | ((O0 & 1) << 5) : odd;
+      // the slot bits of the hand-off store address from the parities of X =
+      // Rm + 1 and Y = Cm + 1 -- (odd ^ 6) << 5, i.e. slot s is stored at
+      // position s ^ 6 (the owner reads there) -- by shift-and-or steps
+      (void)odd;
+      odd_out = ((X << 7) & 0x80) | ((Y << 6) & 0x40) | ((O0 & 1) << 5);
     };
-    auto sample = [&](bool in_range, RecT<PACKED>& out, int& odd_out) {
+    auto sample = [&](bool in_range, RecT& out, int& odd_out) {
       Loc L;
       locate(in_range, L);
       finish(L, out, odd_out);
@@ -526,20 +502,10 @@ descriptor_kernel(DescArgs A) {
       }
     };
     int odd_cur = 0;
-    uint2 qq_cur = make_uint2(0u, 0u);  // PACKED: this owner's 8 bin bytes of the batch
+    uint2 qq_cur = make_uint2(0u, 0u);  // this owner's 8 bin bytes of the batch
     Loc loc_nxt, loc_alt;  // PF = 2: batches k + 1 and k + 2, located and gathering (two buffers)
-    Loc loc_3rd;           // PF = 3: the third buffer
     if (nmax > 0) {
-      if constexpr (PF == 3) {
-        Loc l0;
-        locate(0 < nsq, l0);
-        advance();
-        locate(8 < nsq, loc_nxt);
-        advance();
-        locate(16 < nsq, loc_alt);
-        advance();
-        finish(l0, rc_cur, odd_cur);
-      } else if constexpr (PF == 2) {
+      if constexpr (PF == 2) {
         Loc l0;
         locate(0 < nsq, l0);
         advance();
@@ -554,7 +520,7 @@ descriptor_kernel(DescArgs A) {
     // one batch: ln = batch k + 1 (PF = 2; located a step ago), l2 = the batch
     // located in this step
     auto step = [&](int base, Loc& ln, Loc& l2) {
-      if constexpr (PACKED) {
+      {
         // corner k to owner slot s = k ^ odd: value at byte (g << 8) | ((s ^ 6) << 5) |
         // (q << 2), bit 4 flipped on odd groups (so a 16-lane pass of the
         // owners' ds_read_b128 -- an even and an odd group -- covers all 64
@@ -592,26 +558,19 @@ descriptor_kernel(DescArgs A) {
           p1 = (unsigned)__builtin_amdgcn_mov_dpp((int)w1, 0xB1, 0xf, 0xf, true);
           qq_cur = make_uint2(__builtin_amdgcn_perm(p0, w0, s1), __builtin_amdgcn_perm(p1, w1, s1));
         }
-      } else {
-        float2* dst2 = reinterpret_cast<float2*>(rec + q * kRecStride2 + g * 16);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          dst2[(2 * t) ^ odd_cur] = make_float2(rc_cur.r[t].x, rc_cur.r[t].y);
-          dst2[(2 * t + 1) ^ odd_cur] = make_float2(rc_cur.r[t].z, rc_cur.r[t].w);
-        }
       }
       wave_sync_d();
-      RecT<PACKED> rc_nxt;
+      RecT rc_nxt;
       int odd_nxt = 0;
-      if constexpr (PF >= 2) {
-        locate(base + 8 * PF < nsq, l2);  // batch k + PF: its gather flies for PF steps
+      if constexpr (PF == 2) {
+        locate(base + 16 < nsq, l2);  // batch k + 2: its gather flies for two steps
         advance();
         finish(ln, rc_nxt, odd_nxt);
       } else {
         locate(base + 8 < nsq, l2);  // batch k + 1: finished after this batch's chain
       }
       // ordered accumulation of batch k: lane q applies its record of each sample
-      if constexpr (PACKED) {
+      {
         const char* rb = reinterpret_cast<const char*>(rec);
         const int rv = (g << 8) | ((q ^ 6) << 5);  // slot q at position q ^ 6 (finish's odd_out)  // samples 0-3 at bit 4 = g & 1, samples 4-7 at the other half
         const float4 va = *reinterpret_cast<const float4*>(rb + (rv | ((g & 1) << 4)));
@@ -627,13 +586,6 @@ descriptor_kernel(DescArgs A) {
           float* hp = reinterpret_cast<float*>(reinterpret_cast<char*>(hist) + ab);
           *hp = *hp + vals[jj];
         }
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const float2 e = reinterpret_cast<const float2*>(rec + jj * kRecStride2)[lane];
-          const int a = (__float_as_int(e.x) << 6) + lane;
-          hist[a] = hist[a] + e.y;
-        }
       }
       if constexpr (PF == 1) {
         // batch k + 1's gathered pixel is first used after the chain (an
@@ -647,16 +599,7 @@ descriptor_kernel(DescArgs A) {
       rc_cur = rc_nxt;
       odd_cur = odd_nxt;
     };
-    if constexpr (PF == 3) {
-      // unrolled by three: the three Loc buffers rotate roles
-      for (int base = 0; base < nmax; base += 24) {
-        step(base, loc_nxt, loc_3rd);
-        if (base + 8 >= nmax) break;
-        step(base + 8, loc_alt, loc_nxt);
-        if (base + 16 >= nmax) break;
-        step(base + 16, loc_3rd, loc_alt);
-      }
-    } else if constexpr (PF == 2) {
+    if constexpr (PF == 2) {
       // unrolled by two so the two Loc buffers swap roles instead of being
       // copied (a copy of the gathered pixel would wait for its load)
       for (int base = 0; base < nmax; base += 16) {
@@ -822,18 +765,11 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
   A.desc = desc;
   A.first_octave = first_octave;
   A.err_flag = err_flag;
-  static const bool packed = [] {
-    const char* e = getenv("SIFT_HIP_DESC_PACKED");  // A/B switch between the two record forms
-    return !e || atoi(e) != 0;
-  }();
   // detected keypoints gather two batches ahead (PF = 2): one image of up to
   // kOneImagePx (one_image_variants) is budgeted for 2 waves per SIMD (few
   // waves, latency-bound chains), batches and larger images for kDescWpe;
-  // SIFT_HIP_DESC_DEEP=0 selects the one-ahead form
-  static const bool deep = [] {
-    const char* e = getenv("SIFT_HIP_DESC_DEEP");
-    return !e || atoi(e) != 0;
-  }();
+  // caller keypoints (calDescriptor: any radius, the whole-window walk) run
+  // the general form one batch ahead
 #ifndef SIFT_DESC_GRID_PCT
 #define SIFT_DESC_GRID_PCT 100  // A/B builds only (tools/build_var.sh): the grid as a share of the resident one
 #endif
@@ -842,21 +778,12 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                      dim3(std::max(8, resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192) *     \
                                           SIFT_DESC_GRID_PCT / 800 * 8)),                                           \
                      dim3(64), 0, st, A)
-  if (packed && detected && deep && one_image_variants(L, batch))
-    SIFT_DESC_LAUNCH(true, true, 2, 2);
-#ifdef SIFT_DESC_PF3
-  else if (packed && detected && deep)
-    SIFT_DESC_LAUNCH(true, true, 3, kDescWpe);  // A/B build: gathers three batches ahead
-#else
-  else if (packed && detected && deep)
-    SIFT_DESC_LAUNCH(true, true, 2, kDescWpe);
-#endif
-  else if (packed && detected)
-    SIFT_DESC_LAUNCH(true, true, 1, kDescWpe);
-  else if (packed)
-    SIFT_DESC_LAUNCH(true, false, 1, kDescWpe);
+  if (detected && one_image_variants(L, batch))
+    SIFT_DESC_LAUNCH(true, 2, 2);
+  else if (detected)
+    SIFT_DESC_LAUNCH(true, 2, kDescWpe);
   else
-    SIFT_DESC_LAUNCH(false, false, 1, 1);
+    SIFT_DESC_LAUNCH(false, 1, kDescWpe);
 #undef SIFT_DESC_LAUNCH
 }
 

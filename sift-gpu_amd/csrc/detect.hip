@@ -4,11 +4,11 @@
 // Output order must equal the reference's: octave -> layer -> row -> col ->
 // histogram peak (src/sift.cpp:556-557, 487-491, 525), duplicates kept.  The
 // GPU therefore never appends with atomics:
-//   dog_extrema    -- one workgroup per 64x16 tile of one octave: the four
-//                     DoG planes (+1-pixel halo) are formed in LDS from the
-//                     five Gaussian planes (and written out), then both
-//                     detection layers are tested from LDS; each wave row is
-//                     one ballot -> two 32-bit words of a candidate bitmask;
+//   extrema_walk   -- one wave per 64-column strip of one octave walks a
+//                     chunk of rows: the four DoG rows are formed from the
+//                     five Gaussian planes in an LDS ring, both detection
+//                     layers are tested, and each row's two ballots are two
+//                     32-bit words of a candidate bitmask;
 //   mask_count / scan / mask_expand -- the bitmask's word order is the
 //                     reference's (octave, layer, row, col) order, so an
 //                     exclusive scan of per-chunk popcounts gives every
@@ -77,172 +77,19 @@ long long mask_words_per_image(const Layout& L) { return make_mask(L).w_img; }
 int mask_blocks_per_image(const Layout& L) { return make_mask(L).bpw; }
 
 // ---- pass 1: DoG (src/sift.cpp:280) fused with the 26-neighbour test --------
-constexpr int kExTW = 64, kExTH = 16;
-
-struct TileArgs {
-  Layout L;
-  MaskLayout M;
-  const float* gpyr;
-  float* dog;
-  float2* grad;      // (magnitude, fastAtan2 orientation) of Gaussian layers 1, 2
-  const MathConsts* mc;
-  unsigned* mask;
-  int tile_start[kMaxOctaves + 1];
-  int tiles_x[kMaxOctaves];
-  int write_dog;  // 1: form DoG from the Gaussian planes (not stored); 0: read the DoG planes
-};
-
-// src/sift.cpp:493-511 on an LDS tile: v at (y, x) of plane cur; ties pass.
-__device__ __forceinline__ bool lds_extremum(const float (*lo)[kExTW + 4], const float (*cu)[kExTW + 4],
-                                             const float (*hi)[kExTW + 4], int y, int x) {
-  const float v = cu[y][x];
-  if (!(fabsf(v) > kDogThreshold)) return false;
-  bool ok = true;
-  if (v > 0) {
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        ok = ok && v >= lo[y + dy][x + dx] && v >= hi[y + dy][x + dx];
-        if (dy != 0 || dx != 0) ok = ok && v >= cu[y + dy][x + dx];
-      }
-  } else if (v < 0) {
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        ok = ok && v <= lo[y + dy][x + dx] && v <= hi[y + dy][x + dx];
-        if (dy != 0 || dx != 0) ok = ok && v <= cu[y + dy][x + dx];
-      }
-  } else {
-    ok = false;
-  }
-  return ok;
-}
-
-__global__ __launch_bounds__(256) void dog_extrema_kernel(TileArgs A) {
-  __shared__ float sd[kDogPer][kExTH + 2][kExTW + 4];
-  __shared__ float sg[2][kExTH + 2][kExTW + 4];  // Gaussian layers 1, 2 (for gradients)
-  const int b = blockIdx.y;
-  const int t = blockIdx.x;
-  int o = 0;
-  while (o + 1 < A.L.n_oct && A.tile_start[o + 1] <= t) ++o;
-  const int local = t - A.tile_start[o];
-  const int y0 = (local / A.tiles_x[o]) * kExTH, x0 = (local % A.tiles_x[o]) * kExTW;
-  const Octave& O = A.L.oct[o];
-  const long long pitch = O.pitch;
-  const float* g = A.gpyr + b * A.L.g_img;
-  float* dg = A.dog + b * A.L.d_img;
-  // DoG tile with a one-pixel halo, computed from the five Gaussian planes
-  // (or read, when the caller supplied the DoG pyramid)
-  // Branch-free (clamped addresses, then a select): all 5 items of a lane
-  // have their loads in flight together instead of one HBM round trip each.
-  constexpr int kN = (kExTH + 2) * (kExTW + 2), kIt = (kN + 255) / 256;
-  float ld[kIt][6];
-  bool okv[kIt];
-#pragma unroll
-  for (int u = 0; u < kIt; ++u) {
-    const int i = min((int)threadIdx.x + 256 * u, kN - 1);
-    const int rr = i / (kExTW + 2), cc = i % (kExTW + 2);
-    const int y = y0 - 1 + rr, x = x0 - 1 + cc;
-    okv[u] = y >= 0 && y < O.rows && x >= 0 && x < O.cols;
-    const long long p = (long long)min(max(y, 0), O.rows - 1) * pitch + min(max(x, 0), O.cols - 1);
-    ld[u][0] = g[O.g_off[1] + p];
-    ld[u][1] = g[O.g_off[2] + p];
-    if (A.write_dog) {
-      ld[u][2] = g[O.g_off[0] + p];
-      ld[u][3] = g[O.g_off[3] + p];
-      ld[u][4] = g[O.g_off[4] + p];
-      ld[u][5] = 0.f;
-    } else {
-      ld[u][2] = dg[O.d_off[0] + p];
-      ld[u][3] = dg[O.d_off[1] + p];
-      ld[u][4] = dg[O.d_off[2] + p];
-      ld[u][5] = dg[O.d_off[3] + p];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kIt; ++u) {
-    const int i = threadIdx.x + 256 * u;
-    if (i < kN) {
-      const int rr = i / (kExTW + 2), cc = i % (kExTW + 2);
-      const float g1 = okv[u] ? ld[u][0] : 0.f, g2 = okv[u] ? ld[u][1] : 0.f;
-      float d0, d1, d2, d3;
-      if (A.write_dog) {
-        // Not stored: refinement forms the same differences from the Gaussian
-        // planes (refine_candidate<true>), which saves 16 B/px of HBM writes.
-        const float g0 = okv[u] ? ld[u][2] : 0.f, g3 = okv[u] ? ld[u][3] : 0.f, g4 = okv[u] ? ld[u][4] : 0.f;
-        d0 = g1 - g0;
-        d1 = g2 - g1;
-        d2 = g3 - g2;
-        d3 = g4 - g3;
-      } else {
-        d0 = okv[u] ? ld[u][2] : 0.f;
-        d1 = okv[u] ? ld[u][3] : 0.f;
-        d2 = okv[u] ? ld[u][4] : 0.f;
-        d3 = okv[u] ? ld[u][5] : 0.f;
-      }
-      sd[0][rr][cc] = d0;
-      sd[1][rr][cc] = d1;
-      sd[2][rr][cc] = d2;
-      sd[3][rr][cc] = d3;
-      sg[0][rr][cc] = g1;
-      sg[1][rr][cc] = g2;
-    }
-  }
-  __syncthreads();
-  // Per-pixel gradient of layers 1 and 2 -- the (magnitude, orientation) that
-  // calcOrientationHist (src/sift.cpp:413-426) and calcSIFTDescriptor
-  // (:623-633) evaluate per window sample; both depend on the pixel only.
-  {
-    const AtanConsts ak = A.mc->t;
-    float2* gr = A.grad + b * A.L.g_img;
-    for (int i = threadIdx.x; i < 2 * kExTH * kExTW; i += 256) {
-      const int ls = i / (kExTH * kExTW), rem = i % (kExTH * kExTW);
-      const int rr = rem / kExTW, cc = rem % kExTW;
-      const int y = y0 + rr, x = x0 + cc;
-      if (y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1) {
-        const float(*G)[kExTW + 4] = sg[ls];
-        const float dx = (float)(G[rr + 1][cc + 2] - G[rr + 1][cc]);
-        const float dy = (float)(G[rr][cc + 1] - G[rr + 2][cc + 1]);
-        gr[O.g_off[1 + ls] + (long long)y * pitch + x] = make_float2(magnitude(dx, dy), fast_atan2(dy, dx, ak));
-      }
-    }
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int seg1 = 2 * o, seg2 = 2 * o + 1;
-  const int wpr = A.M.wpr[seg1];
-  for (int rr = wv; rr < kExTH; rr += 4) {
-    const int r = y0 + rr, c = x0 + lane;
-    const bool inside = r >= kBorder && r < O.rows - kBorder && c >= kBorder && c < O.cols - kBorder;
-    const bool f1 = inside && lds_extremum(sd[0], sd[1], sd[2], rr + 1, lane + 1);
-    const bool f2 = inside && lds_extremum(sd[1], sd[2], sd[3], rr + 1, lane + 1);
-    const unsigned long long m1 = __ballot(f1), m2 = __ballot(f2);
-    if (r < O.rows && (lane == 0 || lane == 32)) {
-      const int w = x0 / 32 + (lane >> 5);
-      if (w < wpr) {
-        const long long base = b * A.M.w_img + (long long)r * wpr + w;
-        A.mask[base + A.M.start[seg1]] = (unsigned)(m1 >> lane);
-        A.mask[base + A.M.start[seg2]] = (unsigned)(m2 >> lane);
-      }
-    }
-  }
-}
-
-// ---- pass 1, walking form (default) -----------------------------------------
 // One wave owns a 64-column strip (64-aligned, so its ballots are exactly two
 // mask words per row) of one octave and walks a chunk of rows.  Each row of
 // the five Gaussian planes (or the caller's DoG planes) is loaded once --
 // lanes 0 and 1 also fetch the columns x0-1 and x0+64 -- one row ahead of its
 // use, turned into the four DoG rows + Gaussian layers 1, 2 and put into a
 // three-row LDS ring; row y is then tested and its gradients written as soon
-// as row y+1 is in the ring.  Against the 64x16 tiles above: no 2-row halo
-// per tile (rows are read once per chunk), the loads of the next row fly
-// while the current one is tested, and a wave needs 4.9 KB of LDS instead of
-// a quarter of 29 KB, so 8 waves per SIMD stay resident.  Same values, same
-// bits (the 26-neighbour test only compares; the gradients and DoG are the
-// same float expressions).
+// as row y+1 is in the ring.  Against round 1's 64x16 tiles (a workgroup per
+// tile, 29 KB of LDS, 1.16x the rows with the halo; 2.26 vs 1.56 ms per step,
+// tools/patches/r5_variants.patch): no 2-row halo per tile (rows are read
+// once per chunk), the loads of the next row fly while the current one is
+// tested, and a wave needs 4.9 KB of LDS, so 8 waves per SIMD stay resident.
+// Same values, same bits (the 26-neighbour test only compares; the gradients
+// and DoG are the same float expressions).
 constexpr int kWCols = 64 + 4;  // ring row: column x0 - 1 + c at c (c = 0..65)
 
 struct WalkArgs {
@@ -762,58 +609,34 @@ void launch_grad(hipStream_t st, const Layout& L, const float* gpyr, float2* gra
 
 void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* dog, bool write_dog,
                     float2* grad, const MathConsts* mc, int batch, DetectBufs& D) {
-  TileArgs A;
-  A.L = L;
-  A.M = make_mask(L);
-  A.gpyr = gpyr;
-  A.dog = dog;
-  A.grad = grad;
-  A.mc = mc;
-  A.mask = D.mask;
-  A.write_dog = write_dog ? 1 : 0;
-  int t = 0;
+  WalkArgs W;
+  W.L = L;
+  W.M = make_mask(L);
+  W.gpyr = gpyr;
+  W.dog = dog;
+  W.grad = grad;
+  W.mc = mc;
+  W.mask = D.mask;
+  // rows per wave: about 64 K waves over the launch (measured on the
+  // 64 x 1080p batch: 16 K 1.70 ms, 32 K 1.60, 64 K 1.56), at least 8 rows
+  // (a chunk re-reads 2 rows)
+  long long strip_rows = 0;
+  for (int o = 0; o < L.n_oct; ++o) strip_rows += (long long)((L.oct[o].cols + 63) / 64) * L.oct[o].rows;
+  constexpr long long target = 65536;  // waves per launch (16 K / 32 K / 64 K measured in round 2)
+  W.chunk = (int)std::min<long long>(512, std::max<long long>(8, strip_rows * batch / target));
+  int w = 0;
   for (int o = 0; o < L.n_oct; ++o) {
-    A.tile_start[o] = t;
-    A.tiles_x[o] = (L.oct[o].cols + kExTW - 1) / kExTW;
-    t += A.tiles_x[o] * ((L.oct[o].rows + kExTH - 1) / kExTH);
+    W.wave_start[o] = w;
+    W.strips[o] = (L.oct[o].cols + 63) / 64;
+    w += W.strips[o] * ((L.oct[o].rows + W.chunk - 1) / W.chunk);
   }
-  A.tile_start[L.n_oct] = t;
-  static const bool tiles = [] {
-    const char* e = getenv("SIFT_HIP_EXTREMA_TILES");  // A/B switch: the 64x16 tile kernel
-    return e && atoi(e) != 0;
-  }();
-  if (tiles) {
-    hipLaunchKernelGGL(dog_extrema_kernel, dim3(t, batch), dim3(256), 0, st, A);
-  } else {
-    WalkArgs W;
-    W.L = L;
-    W.M = A.M;
-    W.gpyr = gpyr;
-    W.dog = dog;
-    W.grad = grad;
-    W.mc = mc;
-    W.mask = D.mask;
-    // rows per wave: about 64 K waves over the launch (measured on the
-    // 64 x 1080p batch: 16 K 1.70 ms, 32 K 1.60, 64 K 1.56), at least 8 rows
-    // (a chunk re-reads 2 rows)
-    long long strip_rows = 0;
-    for (int o = 0; o < L.n_oct; ++o) strip_rows += (long long)((L.oct[o].cols + 63) / 64) * L.oct[o].rows;
-    constexpr long long target = 65536;  // waves per launch (16 K / 32 K / 64 K measured in round 2)
-    W.chunk = (int)std::min<long long>(512, std::max<long long>(8, strip_rows * batch / target));
-    int w = 0;
-    for (int o = 0; o < L.n_oct; ++o) {
-      W.wave_start[o] = w;
-      W.strips[o] = (L.oct[o].cols + 63) / 64;
-      w += W.strips[o] * ((L.oct[o].rows + W.chunk - 1) / W.chunk);
-    }
-    W.wave_start[L.n_oct] = w;
-    const int wg = (w + 7) / 8 * 8;  // whole XCD runs (extra waves exit)
-    if (write_dog)
-      hipLaunchKernelGGL(extrema_walk_kernel<true>, dim3(wg, batch), dim3(64), 0, st, W);
-    else
-      hipLaunchKernelGGL(extrema_walk_kernel<false>, dim3(wg, batch), dim3(64), 0, st, W);
-  }
-  const MaskLayout& M = A.M;
+  W.wave_start[L.n_oct] = w;
+  const int wg = (w + 7) / 8 * 8;  // whole XCD runs (extra waves exit)
+  if (write_dog)
+    hipLaunchKernelGGL(extrema_walk_kernel<true>, dim3(wg, batch), dim3(64), 0, st, W);
+  else
+    hipLaunchKernelGGL(extrema_walk_kernel<false>, dim3(wg, batch), dim3(64), 0, st, W);
+  const MaskLayout& M = W.M;
   hipLaunchKernelGGL(mask_count_kernel, dim3(M.bpw, batch), dim3(256), 0, st, D.mask, M.w_img, M.bpw,
                      D.blk_counts);
   const int nblk = M.bpw * batch;
@@ -836,7 +659,6 @@ struct RefArgs {
   int cand_cap;
   CandOut* couts;
   int* npeaks;
-  int* ori_next;  // [8] orient_bin_kernel<true>'s per-XCD candidate counters
 };
 
 // adjustLocalExtrema (src/sift.cpp:287-388) for one candidate.
@@ -993,9 +815,6 @@ __device__ __forceinline__ Refined refine_candidate(const Layout& Lay, const flo
 // Refinement: one lane per candidate.  Writes the refined keypoint fields and
 // the orientation pass's inputs (refined r, c, layer; npeaks = 1 if kept).
 __global__ __launch_bounds__(256) void refine_kernel(RefArgs A) {
-  // the next launch on this stream is the orientation pass: its work counters
-  // start at 0 on every path (graph replay, direct launches, sub-module calls)
-  if (blockIdx.x == 0 && threadIdx.x < 8) A.ori_next[threadIdx.x] = 0;
   int n = *A.cand_total;
   if (n > A.cand_cap) n = A.cand_cap;
   for (int ci = blockIdx.x * 256 + threadIdx.x; ci < n; ci += gridDim.x * 256) {
@@ -1018,198 +837,14 @@ __global__ __launch_bounds__(256) void refine_kernel(RefArgs A) {
   }
 }
 
-// Orientation histograms: eight candidates per wave (lanes 8g..8g+7 own
-// candidate g).  Samples are computed 8 at a time per group and added to the
-// group's 36-bin histogram in raster order, lane q of the group at step q
-// (one plain LDS read-modify-write advances all eight groups' ordered chains;
-// the ds_add_f32 atomic it replaced cost 2.65 vs 2.26 ms per step).
-// Lane balance (speed only): each chunk of 64 consecutive candidates is ranked
-// by window radius (rejected candidates first, radius 0) and each sub-batch
-// takes 8 consecutive ranks, as in descriptor.hip.
+// Orientation: the batch kernel (orient_slots_kernel below) gives each 8-lane
+// group candidates; lanes 8g..8g+7 of a group add their samples to the
+// group's 36-bin histograms in raster order, lane q at step q.
 constexpr int kOGrp = 8;
-constexpr int kOChunk = 64;
-constexpr int kOU = 4;  // sample batches per loop step
 
 __device__ __forceinline__ int ori_radius(float size, int o) {
   const float scl = size * 0.5f / (1 << o);
   return cv_round(3 * 1.5f * scl);
-}
-
-__global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
-  __shared__ float oh[kOGrp][kOriBins + 4];
-  __shared__ float sm[kOGrp][kOriBins + 4];
-  __shared__ int sord[kOGrp];
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 3, q = lane & 7;
-  int n = *A.cand_total;
-  if (n > A.cand_cap) n = A.cand_cap;
-  const ExpConsts ek = A.mc->e;
-  __shared__ float etab[64];  // exp32f table, LDS-resident (gathered per sample)
-  etab[lane] = A.mc->exptab[lane];
-  wave_sync();
-
-  // XCD-aware contiguous split of the raster-ordered candidates (speed only)
-  const int xcd = blockIdx.x & 7, nslot = gridDim.x >> 3, slot = blockIdx.x >> 3;
-  const int per = ((n + 7) / 8 + kOChunk - 1) / kOChunk * kOChunk;
-  const int c0 = xcd * per;
-  const int cend = min(n, (xcd + 1) * per);
-  const int chend = c0 + (max(cend - c0, 0) + kOChunk - 1) / kOChunk * kOChunk;
-  for (int cb = c0 + slot * kOGrp; cb < chend; cb += nslot * kOGrp) {
-    const int rel8 = (cb - c0) / kOGrp, pass = rel8 / nslot;
-    const int kc = c0 + (rel8 / 8) * kOChunk, win = ((rel8 & 7) ^ (pass & 7)) * kOGrp;
-    {
-      const int kk = kc + lane;
-      int key = 0x1ffffff;  // past the end: ranked last
-      if (kk < cend) {
-        const CandOut& co = A.couts[kk];
-        key = co.npeaks ? min(max(ori_radius(co.size, A.cands[kk].ol & 255), 0), 0xffffff) : 0;
-      }
-      key = (key << 6) | lane;
-      int rank = 0;
-#pragma unroll
-      for (int m = 0; m < 64; ++m) rank += __builtin_amdgcn_readlane(key, m) < key ? 1 : 0;
-      if (rank >= win && rank < win + kOGrp) sord[rank - win] = kk;
-      wave_sync();
-    }
-    const int ci = sord[g];
-    bool ok = false;
-    int o = 0, rr = 0, rc = 0, rl = 0, b = 0;
-    float size = 0.f;
-    if (ci < cend) {
-      const CandOut& co = A.couts[ci];
-      ok = co.npeaks != 0;
-      o = A.cands[ci].ol & 255;
-      size = co.size;
-      rr = co.ref_r;
-      rc = co.ref_c;
-      rl = co.ref_layer;
-      b = co.img;
-    }
-    const Octave& O = A.L.oct[o];
-    const long long pitch = O.pitch;
-    // ---- calcOrientationHist, src/sift.cpp:389-458 ----
-    const float scl = size * 0.5f / (1 << o);
-    const int radius = ok ? cv_round(3 * 1.5f * scl) : 0;
-    const float sigma = 1.5f * scl;
-    const float escale = -1.f / (2.f * sigma * sigma);
-    const float2* gimg = A.grad + b * A.L.g_img + O.g_off[ok ? rl : 0];
-    const int D = 2 * radius + 1;
-    const int ns = ok ? D * D : 0;
-    for (int t = q; t < kOriBins; t += 8) oh[g][t] = 0.f;
-    int nmax = ns;
-    nmax = max(nmax, __shfl_xor(nmax, 8));
-    nmax = max(nmax, __shfl_xor(nmax, 16));
-    nmax = max(nmax, __shfl_xor(nmax, 32));
-    wave_sync();
-    // lane q walks samples s = q, q+8, ... as (row si, column sj) of the window
-    const int Dw = ns ? D : 0x40000000;  // rejected: never wraps
-    int si = 0, sj = q;
-    while (sj >= Dw) {
-      sj -= Dw;
-      ++si;
-    }
-    // kOU batches of 8 samples per step: the kOU gathers are issued together
-    // (branch-free, clamped address), then the adds run in sample order.
-    for (int base = 0; base < nmax; base += 8 * kOU) {
-      float2 mo[kOU];
-      int ii[kOU], jv[kOU];
-      bool okv[kOU];
-#pragma unroll
-      for (int u = 0; u < kOU; ++u) {
-        const int i = si - radius, j = sj - radius;
-        sj += 8;
-        while (sj >= Dw) {
-          sj -= Dw;
-          ++si;
-        }
-        const int y = rr + i, x = rc + j;
-        okv[u] = base + 8 * u + q < ns && y > 0 && y < O.rows - 1 && x > 0 && x < O.cols - 1;
-        ii[u] = i;
-        jv[u] = j;
-        mo[u] = gimg[okv[u] ? (long long)y * pitch + x : 0];  // (Mag, Ori) of the pixel
-      }
-#pragma unroll
-      for (int u = 0; u < kOU; ++u) {
-        const float w = exp32f((ii[u] * ii[u] + jv[u] * jv[u]) * escale, etab, ek);
-        int bin = cv_round((kOriBins / 360.f) * mo[u].y);
-        if (bin >= kOriBins) bin -= kOriBins;
-        if (bin < 0) bin += kOriBins;
-        const float val = w * mo[u].x;
-        // step jj: lane jj of every group adds its sample into its group's
-        // histogram -- a plain read-modify-write (one lane per group, groups
-        // own disjoint rows; the wave's LDS operations stay in program order,
-        // so step jj + 1 reads what step jj wrote).  As in orient_slots_kernel,
-        // each step tests a fresh opaque copy of q behind a compiler barrier:
-        // eight plain `q == jj` blocks are mutually exclusive for one thread,
-        // and hipcc once rebuilt them as a switch and ran the steps out of
-        // order (tools/check_orient_isa.py checks the compiled steps).
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          int qv = q;
-          asm volatile("; orient step %1" : "+v"(qv) : "n"(jj) : "memory");
-          if (qv == jj && okv[u]) {
-            const float h = oh[g][bin];
-            oh[g][bin] = h + val;
-          }
-        }
-      }
-    }
-    wave_sync();
-    // smoothing (src/sift.cpp:440-451), max, peaks (src/sift.cpp:524-541)
-    float mx = -1.f;
-    for (int t = q; t < kOriBins; t += 8) {
-      const float* th = oh[g];
-      const int jm2 = (t + kOriBins - 2) % kOriBins, jp2 = (t + 2) % kOriBins;
-      const int jm1 = (t + kOriBins - 1) % kOriBins, jp1 = (t + 1) % kOriBins;
-      const float h = (th[jm2] + th[jp2]) * (1.f / 16.f) + (th[jm1] + th[jp1]) * (4.f / 16.f) +
-                      th[t] * (6.f / 16.f);
-      sm[g][t] = h;
-      mx = fmaxf(mx, h);
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 1));
-    mx = fmaxf(mx, __shfl_xor(mx, 2));
-    mx = fmaxf(mx, __shfl_xor(mx, 4));
-    wave_sync();
-    const float mag_thr = (float)(mx * 0.8f);
-    unsigned long long pmask = 0;
-    float ang[5];
-#pragma unroll
-    for (int m = 0; m < 5; ++m) {
-      const int t = q + 8 * m;
-      ang[m] = 0.f;
-      if (t < kOriBins && ok) {
-        const int l = t > 0 ? t - 1 : kOriBins - 1;
-        const int rr = t < kOriBins - 1 ? t + 1 : 0;
-        const float h = sm[g][t], hl = sm[g][l], hr = sm[g][rr];
-        if (h > hl && h > hr && h >= mag_thr) {
-          float bin = t + 0.5f * (hl - hr) / (hl - 2 * h + hr);
-          bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
-          float a = 360.f - (float)((360.f / kOriBins) * bin);
-          if (fabsf(a - 360.f) < FLT_EPSILON) a = 0.f;
-          ang[m] = a;
-          pmask |= 1ull << t;
-        }
-      }
-    }
-    // OR-reduce the group's peak mask (lanes of a group own disjoint bins)
-    pmask |= __shfl_xor(pmask, 1);
-    pmask |= __shfl_xor(pmask, 2);
-    pmask |= __shfl_xor(pmask, 4);
-    if (ci < cend) {
-      CandOut* co = A.couts + ci;
-#pragma unroll
-      for (int m = 0; m < 5; ++m) {
-        const int t = q + 8 * m;
-        if (t < kOriBins && ((pmask >> t) & 1ull))
-          co->angle[__popcll(pmask & ((1ull << t) - 1ull))] = ang[m];
-      }
-      // co->npeaks keeps the refine pass's kept flag: other waves rank this
-      // chunk from it; the peak count goes to A.npeaks only
-      const int np = ok ? __popcll(pmask) : 0;
-      if (q == 0) A.npeaks[ci] = np;
-    }
-    wave_sync();
-  }
 }
 
 // Orientation histograms, one wave per candidate, bins bucketed (round 4;
@@ -1217,7 +852,7 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
 //
 // The reference's only ordering constraint (src/sift.cpp:429-437) is that each
 // bin receives its terms in window raster order; different bins are
-// independent chains.  orient_kernel walks a window one sample per step
+// independent chains.  The batch kernel walks a window one sample per step
 // (8 samples per batch, each added after the previous one's LDS round trip),
 // so a radius-17 window is a 1,225-step chain and one image's launch is as
 // long as its longest such walk.  Here a wave takes a candidate and 64
@@ -1230,14 +865,11 @@ __global__ __launch_bounds__(64) void orient_kernel(RefArgs A) {
 // exactly the reference's adds in the reference's order.  Invalid samples
 // (outside the image interior, src/sift.cpp:405,410) join no bin; the masked
 // reads past a bin's count add +0.0 to a sum that is >= +0 (exact no-op).
-// DYN (speed only): each wave draws its next candidate of the XCD's range from
-// a per-XCD counter (A.ori_next, zeroed by refine_kernel, the launch before
-// this one on every path) instead of the fixed interleave ci += nw; the draw
-// for the next candidate is issued at the top of the body, so a rejected
-// candidate's `continue` still moves on, and every draw strictly increases.
+// (A per-XCD dynamic candidate fetch was bit-exact and 16 % slower: each
+// draw is a returning atomic that sits in vmcnt order ahead of the
+// candidate's gathers; tools/patches/r5_variants.patch.)
 constexpr int kOBW = 4;  // waves per workgroup
 
-template <bool DYN>
 __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   __shared__ float vals[kOBW][64][kOriBins];  // [wave][rank][bin]: owner reads are conflict free
   __shared__ int cnt[kOBW][64];
@@ -1255,11 +887,7 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   const int per = (n + 7) / 8;
   const int xcd = blockIdx.x & 7, wid = (int)(blockIdx.x >> 3) * kOBW + w;
   const int c0 = xcd * per, cend = min(n, c0 + per);
-  int nxt = 0;
-  if (DYN && lane == 0) nxt = atomicAdd(&A.ori_next[xcd], 1);
-  for (int ci = c0 + (DYN ? __builtin_amdgcn_readfirstlane(nxt) : wid); ci < cend;
-       ci = DYN ? c0 + __builtin_amdgcn_readfirstlane(nxt) : ci + nw) {
-    if (DYN && lane == 0) nxt = atomicAdd(&A.ori_next[xcd], 1);
+  for (int ci = c0 + wid; ci < cend; ci += nw) {
     const CandOut& co = A.couts[ci];
     if (co.npeaks == 0) {  // refinement rejected it
       if (lane == 0) A.npeaks[ci] = 0;
@@ -1278,7 +906,8 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
     // the window's valid rectangle (y in [1, rows - 2], x in [1, cols - 2],
     // src/sift.cpp:405,410): the pixels the reference skips are not
     // enumerated, so the rest keep their raster order and a sample needs no
-    // range test; a kept candidate lies >= 5 px inside, so it is >= 14 wide
+    // range test (a kept candidate lies >= 5 px inside, so the rectangle is
+    // >= min(rad + 5, cols - 2) >= 9 columns wide)
     const int i0 = max(0, 1 - rr + radius), i1 = min(D - 1, O.rows - 2 - rr + radius);
     const int j0 = max(0, 1 - rc + radius), j1 = min(D - 1, O.cols - 2 - rc + radius);
     const int W = max(j1 - j0 + 1, 1), ns = max(j1 - j0 + 1, 0) * max(i1 - i0 + 1, 0);
@@ -1388,8 +1017,8 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
 
 // Orientation histograms, kOSlots candidates per lane group (default kernel).
 //
-// orient_kernel above is bound by its histogram chain: a group's 8 samples of a
-// batch are applied one after the other (each read-modify-write waits for the
+// One candidate per group (round 1's orient_kernel) is bound by its histogram
+// chain: a group's 8 samples of a batch are applied one after the other (each read-modify-write waits for the
 // previous one's LDS round trip, ~100 cycles), and a wave's run time is the
 // sum of its chains, which more resident waves cannot shorten.  Here each
 // group carries kOSlots candidates at once -- 8 x kOSlots per wave -- with one
@@ -1489,8 +1118,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOSlots == 2
       const int j0 = max(0, 1 - rc + rad), j1 = min(D - 1, O.cols - 2 - rc + rad);
       const int wv = j1 - j0 + 1, hv = i1 - i0 + 1;
       ns[u] = ok && wv > 0 && hv > 0 ? wv * hv : 0;
-      // a kept candidate lies >= 5 px inside its octave and rad >= 9, so wv >= 14
-      // > 8: one advance wraps at most once; rejected: never wraps
+      // a kept candidate lies >= 5 px inside its octave (cols >= 11) and
+      // rad = cvRound(4.5 scl) >= 8, so wv >= min(rad + 5, cols - 2) >= 9 > 8:
+      // one advance wraps at most once; rejected: never wraps
       Dw[u] = ns[u] ? wv : 0x40000000;
       jend[u] = ns[u] ? j1 + 1 : 0x40000000;
       // lane q walks samples s = q, q+8, ... as (row si, column sj) of the rectangle
@@ -1655,41 +1285,16 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   A.cand_cap = D.cand_cap;
   A.couts = D.couts;
   A.npeaks = D.npeaks;
-  A.ori_next = D.ori_next;
   hipLaunchKernelGGL(refine_kernel, dim3(resident_grid((const void*)refine_kernel, 256, 0, 2048)), dim3(256), 0, st, A);
-  // batches: two candidates per lane group (orient_slots_kernel<2>); one
-  // image: one wave per candidate with bucketed bins (orient_bin_kernel,
-  // round 4), whose chain is a window's largest per-batch bin counts instead
-  // of its whole sample walk.  SIFT_HIP_ORIENT_SLOTS=1 (orient_kernel),
-  // 2..4 (orient_slots_kernel<n>) or 5 (orient_bin_kernel) forces a variant
-  // (A/B runs; every variant is bit-identical, tests/test_gpu_parity.py)
-  static const int slots_env = [] {
-    const char* e = getenv("SIFT_HIP_ORIENT_SLOTS");
-    const int v = e ? atoi(e) : 0;
-    return v >= 1 && v <= 5 ? v : 0;
-  }();
-  const int slots = slots_env ? slots_env : one_image_variants(L, batch) ? 5 : 2;
-  static const bool dyn = [] {
-    const char* e = getenv("SIFT_HIP_ORIENT_DYN");  // A/B: per-XCD work counters in orient_bin_kernel
-    return e && atoi(e) != 0;
-  }();
-  if (slots == 5 && dyn)
-    hipLaunchKernelGGL(orient_bin_kernel<true>,
-                       dim3(resident_grid((const void*)orient_bin_kernel<true>, 64 * kOBW, 0, 2048)), dim3(64 * kOBW),
-                       0, st, A);
-  else if (slots == 5)
-    hipLaunchKernelGGL(orient_bin_kernel<false>,
-                       dim3(resident_grid((const void*)orient_bin_kernel<false>, 64 * kOBW, 0, 2048)), dim3(64 * kOBW),
-                       0, st, A);
-  else if (slots == 1)
-    hipLaunchKernelGGL(orient_kernel, dim3(resident_grid((const void*)orient_kernel, 64, 0, 8192)), dim3(64), 0, st,
-                       A);
-  else if (slots == 3)
-    hipLaunchKernelGGL(orient_slots_kernel<3>,
-                       dim3(resident_grid((const void*)orient_slots_kernel<3>, 64, 0, 8192)), dim3(64), 0, st, A);
-  else if (slots == 4)
-    hipLaunchKernelGGL(orient_slots_kernel<4>,
-                       dim3(resident_grid((const void*)orient_slots_kernel<4>, 64, 0, 8192)), dim3(64), 0, st, A);
+  // batches: two candidates per lane group (orient_slots_kernel<2>; three
+  // slots 1.65, four 1.53-1.57 vs 1.48-1.50 ms, round 5); one image: one wave
+  // per candidate with bucketed bins (orient_bin_kernel, round 4), whose chain
+  // is a window's largest per-batch bin counts instead of its whole sample
+  // walk.  Every variant is bit-identical (the losers are kept as
+  // tools/patches/r5_variants.patch).
+  if (one_image_variants(L, batch))
+    hipLaunchKernelGGL(orient_bin_kernel, dim3(resident_grid((const void*)orient_bin_kernel, 64 * kOBW, 0, 2048)),
+                       dim3(64 * kOBW), 0, st, A);
   else
     hipLaunchKernelGGL(orient_slots_kernel<2>,
                        dim3(resident_grid((const void*)orient_slots_kernel<2>, 64, 0, 8192)), dim3(64), 0, st, A);

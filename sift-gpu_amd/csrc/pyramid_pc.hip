@@ -6,15 +6,14 @@
 // octave base with the reference's sigma, width floor(3 sigma) (:97) and zero
 // padding outside [0, rows-1) x [0, cols-1) (:116)) in exactly the operation
 // order of oracle/sift_oracle.c's so_fast_pyramid, so the planes are its bits
-// (tests/test_gpu_fast.py) -- and those of round 3-4's pyramid_tri.hip, which
-// this file replaces (git history keeps it).
+// (tests/test_gpu_fast.py).
 //
-// Why (profiles/r5_tri_stamps.txt, r5_tri_ablation.txt): pyramid_tri.hip's
-// three roles met at one s_barrier per step; role 0 (w = 18) waited there 37 %
+// Why this structure (profiles/r5_tri_stamps.txt, r5_tri_ablation.txt): the
+// previous kernel's three roles (rounds 3-4, removed; git history at commit
+// 319d385) met at one s_barrier per step; role 0 (w = 18) waited there 37 %
 // of its time while the io roles ran the octave-0 base blur, and the io roles'
 // vmcnt wait for their own source rows also waited for every older plane
-// store.  With no FMAs at all that kernel still took 1.06 ms per 64 x 1080p
-// step (memory + LDS skeleton), with no memory 1.04 ms.
+// store.
 //
 //  * Workgroup = 4 waves over a 64-column strip and a chunk of rows, 8 rows
 //    per step:
@@ -155,10 +154,10 @@ __device__ __forceinline__ int pc_peek(const int* w) {
 }
 // Wait until *w >= v (bounded); then the caller's later LDS reads see what was
 // written before the matching publish.
-__device__ __forceinline__ void pc_wait_ge(const int* w, int v, int* err) {
+__device__ __forceinline__ void pc_wait_ge(const int* w, int v, int* err, int poll_max) {
   int it = 0;
   while (pc_peek(w) < v) {
-    if (++it > kPollMax) {
+    if (++it > poll_max) {
       if ((threadIdx.x & 63) == 0) atomicOr(err, 1);
       break;
     }
@@ -166,10 +165,10 @@ __device__ __forceinline__ void pc_wait_ge(const int* w, int v, int* err) {
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
-__device__ __forceinline__ void pc_wait_done(const PcFlags& f, int v, int* err) {
+__device__ __forceinline__ void pc_wait_done(const PcFlags& f, int v, int* err, int poll_max) {
   int it = 0;
   while (min(min(pc_peek(&f.done[0]), pc_peek(&f.done[1])), pc_peek(&f.done[2])) < v) {
-    if (++it > kPollMax) {
+    if (++it > poll_max) {
       if ((threadIdx.x & 63) == 0) atomicOr(err, 1);
       break;
     }
@@ -292,6 +291,7 @@ namespace {
 // s % kPD (zero outside [0, rows-1) x [0, cols-1): getSubMatrix applied to the
 // base as the scales' source) and plane 0 (columns [x0, x0 + 64), rows
 // [y0, y1)).  Step -1 runs the row pass only (hb rows [Ys0 - 4, Ys0 + 4)).
+template <int kPoll>
 __device__ __forceinline__ void pc_producer0(const PcArgs& A, PcLds0& L, int b, int x0, int y0, int y1) {
   const int lane = threadIdx.x & 63;
   const int rows = A.rows, cols = A.cols;
@@ -383,7 +383,7 @@ __device__ __forceinline__ void pc_producer0(const PcArgs& A, PcLds0& L, int b, 
     if (s + 1 < nsteps) issue(s + 1);  // into the slot step s - 1 used (its row pass is done)
     row_pass(s);
     // slot s % kPD is free once every consumer has read step s - kPD
-    pc_wait_done(L.f, s - kPD + 1, A.err);
+    pc_wait_done(L.f, s - kPD + 1, A.err, kPoll);
     pc_wave_sync();
     float* const bslot = &L.base[s % kPD][0][0];
     // column pass: lane = base column bc (100: lanes 0-63, then 0-35), all
@@ -433,6 +433,7 @@ __device__ __forceinline__ void pc_producer0(const PcArgs& A, PcLds0& L, int b, 
 
 // ---- producer, octave > 0: plane-0 rows by LDS-DMA straight into the ring,
 // two steps ahead ----
+template <int kPoll>
 __device__ __forceinline__ void pc_producerN(const PcArgs& A, PcLdsN& L, int b, int x0, int y0, int y1) {
   const int lane = threadIdx.x & 63;
   const int rows = A.rows, cols = A.cols;
@@ -470,7 +471,7 @@ __device__ __forceinline__ void pc_producerN(const PcArgs& A, PcLdsN& L, int b, 
     // every octave > 0 -- profiles/r5_pc_stamps.txt -- while this wave idles)
     // into h18 slot s % kPH18, read by consumer 0 as lane = column 4i + R
     if (Ys + kPB - 1 + kPH >= y0 && Ys - kPH < y1) {
-      pc_wait_ge(&L.f.hdone, s - kPH18 + 1, A.err);
+      pc_wait_ge(&L.f.hdone, s - kPH18 + 1, A.err, kPoll);
       const float* brow = &L.base[s % kPD][lane >> 4][4 * (lane & 15)];
       float* hs = &L.h18[s % kPH18][0][0];
 #pragma unroll
@@ -484,14 +485,14 @@ __device__ __forceinline__ void pc_producerN(const PcArgs& A, PcLdsN& L, int b, 
     }
     pc_publish(&L.f.hpub, s + 1);
     if (s + 2 < nsteps) {
-      pc_wait_done(L.f, s + 2 - kPD + 1, A.err);  // slot (s + 2) % kPD free
+      pc_wait_done(L.f, s + 2 - kPD + 1, A.err, kPoll);  // slot (s + 2) % kPD free
       issue(s + 2);
     }
   }
 }
 
 // ---- consumer C: its scales over the strip, reading the ring ----
-template <bool OCT0, int C, class LdsT>
+template <bool OCT0, int C, int kPoll, class LdsT>
 __device__ __forceinline__ void pc_consumer(const PcArgs& A, LdsT& L, int b, int x0, int y0, int y1) {
   using R_ = PcRole<C>;
   constexpr int W1 = R_::W1, W2 = R_::W2, P1 = R_::P1, P2 = R_::P2, NC = R_::NC;
@@ -527,12 +528,12 @@ __device__ __forceinline__ void pc_consumer(const PcArgs& A, LdsT& L, int b, int
       float c1[kPB], c2[kPB], o1[kPB], o2[kPB];
       if constexpr (!OCT0 && C == 0) {
         // octaves > 0: the producer ran this scale's row pass (pc_producerN)
-        pc_wait_ge(&L.f.hpub, s + 1, A.err);
+        pc_wait_ge(&L.f.hpub, s + 1, A.err, kPoll);
         const float* hs = &reinterpret_cast<PcLdsN&>(L).h18[s % kPH18][0][0];
 #pragma unroll
         for (int j = 0; j < kPB; ++j) c1[j] = hs[j * kPW + lane];
       } else {
-      pc_wait_ge(&L.f.pub, s + 1, A.err);
+      pc_wait_ge(&L.f.pub, s + 1, A.err, kPoll);
       const float* brow = &L.base[s % kPD][lane >> 4][4 * (lane & 15)];
       // ---- row pass (lane = row R, 4 columns), two rounds of 4 rows, turned
       // into lane = column 4i + R by the register transpose ----
@@ -588,7 +589,11 @@ __device__ __forceinline__ void pc_consumer(const PcArgs& A, LdsT& L, int b, int
   if constexpr (!OCT0 && C == 0) pc_publish(&L.f.hdone, 1 << 30);
 }
 
-template <bool OCT0>
+// kPoll: the bound of every LDS-counter wait -- kPollMax, or 0 for the test
+// hook pc_stall_once (every wait that is not already satisfied expires: the
+// stall path without a hang; a separate instance, so the shipped ones keep
+// their registers and vmcnt accounting, tools/check_pc_isa.py)
+template <bool OCT0, int kPoll = kPollMax>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void pyr_pc_kernel(PcArgs A) {
   __shared__ __attribute__((aligned(16))) char lds[OCT0 ? sizeof(PcLds0) : sizeof(PcLdsN)];
   using LdsT = typename std::conditional<OCT0, PcLds0, PcLdsN>::type;
@@ -622,16 +627,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void p
   __syncthreads();  // the one workgroup barrier: counters initialised
   if (wv == 0) {
     if constexpr (OCT0)
-      pc_producer0(A, L, b, x0, y0, y1);
+      pc_producer0<kPoll>(A, L, b, x0, y0, y1);
     else
-      pc_producerN(A, L, b, x0, y0, y1);
+      pc_producerN<kPoll>(A, L, b, x0, y0, y1);
     PC_WAIT_VM(0);  // the last loads land before the wave ends
   } else if (wv == 1) {
-    pc_consumer<OCT0, 0>(A, L, b, x0, y0, y1);
+    pc_consumer<OCT0, 0, kPoll>(A, L, b, x0, y0, y1);
   } else if (wv == 2) {
-    pc_consumer<OCT0, 1>(A, L, b, x0, y0, y1);
+    pc_consumer<OCT0, 1, kPoll>(A, L, b, x0, y0, y1);
   } else {
-    pc_consumer<OCT0, 2>(A, L, b, x0, y0, y1);
+    pc_consumer<OCT0, 2, kPoll>(A, L, b, x0, y0, y1);
   }
 }
 
@@ -738,7 +743,8 @@ FastPlan fast_plan(int columns, int rows, int slots, int halo) {
 // Octave o of the pyramid, all five planes, and the next octave's plane 0 when
 // it is an exact half (pyramid_fuses_decimation).  src: octave 0's input
 // images (ignored for o > 0: the source is plane 0 of octave o).
-void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch, int* err) {
+void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plane src, int batch, int* err,
+                       bool stall_test) {
   const Octave& O = L.oct[o];
   PcArgs A{};
   A.gpyr = gpyr;
@@ -776,7 +782,11 @@ void launch_pyramid_pc(hipStream_t st, const Layout& L, int o, float* gpyr, Plan
   A.grid_full = (A.n_full + 7) / 8 * 8;
   const long long rest = (long long)(A.columns - A.n_full) * A.chunks;
   const int grid = A.grid_full + (int)((rest + 7) / 8 * 8);
-  if (o > 0)
+  if (stall_test && o > 0)
+    hipLaunchKernelGGL((pyr_pc_kernel<false, 0>), dim3(grid), dim3(256), 0, st, A);
+  else if (stall_test)
+    hipLaunchKernelGGL((pyr_pc_kernel<true, 0>), dim3(grid), dim3(256), 0, st, A);
+  else if (o > 0)
     hipLaunchKernelGGL((pyr_pc_kernel<false>), dim3(grid), dim3(256), 0, st, A);
   else
     hipLaunchKernelGGL((pyr_pc_kernel<true>), dim3(grid), dim3(256), 0, st, A);

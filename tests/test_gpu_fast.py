@@ -191,14 +191,14 @@ def test_fast_batch_equals_single(fctx, oracle, B, R, C):
 @pytest.mark.parametrize("shape,b", [((203, 157), 2), ((540, 960), 5), ((257, 4100), 7)])
 def test_pitch_padding_is_never_read(siftgpu, oracle, monkeypatch, flags, shape, b):
     """the fast pyramid's wide stores leave unspecified values in
-    the pitch padding (common.hpp, kPitchAlign).  With SIFT_HIP_POISON_PAD=1
-    the library writes a NaN into every padding column of every plane after
-    the pyramid; the detect + describe output must not change, in fast and
-    exact mode (shapes with padding at every octave)."""
+    the pitch padding (common.hpp, kPitchAlign).  With the test hook
+    SIFT_HIP_TEST_HOOKS=poison_pad the library writes a NaN into every padding
+    column of every plane after the pyramid; the detect + describe output must
+    not change, in fast and exact mode (shapes with padding at every octave)."""
     img = oracle.synth_image(b, *shape)
     out = []
-    for poison in ("0", "1"):
-        monkeypatch.setenv("SIFT_HIP_POISON_PAD", poison)   # read at context creation
+    for poison in ("", "poison_pad"):
+        monkeypatch.setenv("SIFT_HIP_TEST_HOOKS", poison)   # read at context creation
         ctx = siftgpu.Context(*shape, 1, device=0, flags=flags)
         try:
             out.append(ctx.SIFT_NCL(img))
@@ -238,3 +238,28 @@ def test_fast_headline_batch_equals_single(siftgpu):
     finally:
         ctx.close()
         one.close()
+
+
+def test_expired_pipeline_wait_is_reported_once(siftgpu, oracle, monkeypatch):
+    """pyr_pc_kernel's bounded LDS-counter waits.  The test hook
+    pc_stall_once gives the context's next launch a wait bound of zero, so its
+    waves give up at their first unpublished counter (garbage planes, no
+    hang); buildGaussianPyramid must report SIFT_E_HIP for that call, consume
+    the sticky bit, and the next call must be clean and equal the oracle."""
+    shape, b = (300, 210), 3
+    img = oracle.synth_image(b, *shape)
+    monkeypatch.setenv("SIFT_HIP_TEST_HOOKS", "pc_stall_once")   # read at context creation
+    ctx = siftgpu.Context(*shape, 1, device=0, flags=FAST)
+    try:
+        with pytest.raises(siftgpu.SiftError) as ex:
+            ctx.buildGaussianPyramid(img, 5)
+        assert ex.value.code == siftgpu.SIFT_E_HIP and "wait expired" in str(ex.value)
+        gp = ctx.buildGaussianPyramid(img, 5)           # the bit was consumed: clean
+        ctx.sync()                                      # and nothing left for the sticky report
+        kps, _ = ctx.SIFT_NCL(img)
+    finally:
+        ctx.close()
+    ref = oracle.split_planes(oracle.fast_pyramid(img, 5), *shape, 5, 5)
+    for i, (a, c) in enumerate(zip(gp, ref)):
+        assert a.tobytes() == c.tobytes(), f"plane {i} after the stalled call"
+    assert len(kps) > 0
