@@ -138,6 +138,58 @@ int sift_detect_compute_batch(sift_ctx* ctx, const float* d_imgs, int batch, int
 int sift_synth_images(sift_ctx* ctx, float* d_out, int batch, int rows, int cols,
                       size_t row_stride, size_t img_stride, int seed_base);
 
+/* ---- multi-GPU batch mode (BASELINE configs[3]) ----------
+ * The reference's only parallelism is OpenMP over descriptors
+ * (src/sift.cpp:738); here the images of a batch are sharded over the GPUs of
+ * one node by contiguous ranges, each device runs sift_detect_compute_batch on
+ * its shard, and the keypoint records are gathered to the first device over
+ * RCCL (ncclSend / ncclRecv, xGMI) one step behind the compute.  One process
+ * drives every device (ncclCommInitAll); a multi context is not thread-safe. */
+typedef struct sift_multi sift_multi;
+/* Shard arithmetic: device `index` of n takes the contiguous images
+ * [*first, *first + *count) = [floor(index * batch / n), floor((index + 1) * batch / n)).
+ * No GPU needed. */
+int sift_multi_shard(int batch, int n_devices, int index, int* first, int* count);
+/* Global per-image offsets [sum(counts) + 1] from each shard's own offsets
+ * [counts[i] + 1] (records concatenated in device order).  No GPU needed. */
+int sift_multi_merge_offsets(const int* const* shard_offsets, const int* counts, int n_devices,
+                             int* global_offsets);
+/* One sift_ctx (own HIP stream) per device, two result slots of
+ * kp_cap_per_device records per device, a gather stream per device, the
+ * gather buffers on devices[0] (n_devices x kp_cap_per_device records, and
+ * descriptors when gather_desc), and RCCL communicators over the devices.
+ * Device indices must be distinct (RCCL: one rank per device). */
+int sift_multi_create(const int* devices, int n_devices, int max_rows, int max_cols, int max_batch_per_device,
+                      unsigned flags, int kp_cap_per_device, int gather_desc, sift_multi** out);
+int sift_multi_destroy(sift_multi* m);
+const char* sift_multi_last_error(const sift_multi* m);
+/* The context of device index i (flags, octaves, sift_synth_images, ...). */
+sift_ctx* sift_multi_context(sift_multi* m, int index);
+/* One step: device i detects + describes counts[i] images resident on it
+ * (d_imgs[i], strides in elements as in sift_detect_compute_batch) into its
+ * result slot, and the previous step's records are gathered to devices[0].
+ * Asynchronous, except that the host waits for the previous step's per-image
+ * offsets (one step behind, so normally without blocking). */
+int sift_multi_step(sift_multi* m, const float* const* d_imgs, const int* counts, int rows, int cols,
+                    size_t row_stride, size_t img_stride);
+/* Gathers the last step, drains every stream and reports the contexts' sticky
+ * status (as sift_sync). */
+int sift_multi_flush(sift_multi* m);
+/* The last gathered step on devices[0]: device pointers to its records (and
+ * descriptors, or NULL without gather_desc) in global image order, and the
+ * global per-image offsets [batch_total + 1] into host memory (offsets may be
+ * NULL).  Valid until the next sift_multi_step. */
+int sift_multi_gathered(sift_multi* m, const sift_keypoint** d_kpts, const float** d_desc, int* offsets,
+                        int offsets_cap, int* batch_total, long long* step);
+/* Host copy of the last gathered step's records (and descriptors, desc may be
+ * NULL): *n_out gets the record count; SIFT_E_CAPACITY if cap < count.
+ * Synchronous. */
+int sift_multi_copy_gathered(sift_multi* m, sift_keypoint* kpts, float* desc, int cap, int* n_out);
+/* Steps enqueued, records gathered and p2p transfers posted so far. */
+int sift_multi_stats(const sift_multi* m, long long* steps, long long* records, long long* transfers);
+/* RCCL's NCCL_VERSION_CODE at run time (ncclGetVersion), -1 on error. */
+int sift_multi_rccl_version(void);
+
 /* ---- sub-module entry points (host memory, synchronous) ----------------- */
 /* Gaussian_Blur (include/sift.hpp:47, src/sift.cpp:123-153). */
 int sift_gaussian_blur(sift_ctx* ctx, const float* src, int rows, int cols, double sigma,

@@ -29,7 +29,8 @@ KP_WORDS = 7  # 28-byte cv::KeyPoint record as 7 int32 words
 
 
 def shard(total: int, world: int, rank: int) -> tuple[int, int]:
-    """Contiguous block of images [start, end) owned by `rank` (image b -> rank floor(b*W/B))."""
+    """Contiguous block of images [start, end) = [floor(rank B / W), floor((rank + 1) B / W))
+    owned by `rank` (the C ABI's sift_multi_shard)."""
     return total * rank // world, total * (rank + 1) // world
 
 

@@ -107,6 +107,20 @@ def lib():
             "sift_perspective_transform": (ip, [ctypes.POINTER(ctypes.c_double), fp, ip, fp]),
             "sift_bgr8_to_gray_device": (ip, [vp, vp, ip, ip, ip, sz, sz, ip, ip, vp, sz, sz]),
             "sift_knn_match_l1_device": (ip, [vp, vp, ip, vp, ip, ip, vp, vp]),
+            "sift_multi_shard": (ip, [ip, ip, ip, pint, pint]),
+            "sift_multi_merge_offsets": (ip, [ctypes.POINTER(pint), pint, ip, pint]),
+            "sift_multi_create": (ip, [pint, ip, ip, ip, ip, ctypes.c_uint, ip, ip, ctypes.POINTER(vp)]),
+            "sift_multi_destroy": (ip, [vp]),
+            "sift_multi_last_error": (ctypes.c_char_p, [vp]),
+            "sift_multi_context": (vp, [vp, ip]),
+            "sift_multi_step": (ip, [vp, ctypes.POINTER(vp), pint, ip, ip, sz, sz]),
+            "sift_multi_flush": (ip, [vp]),
+            "sift_multi_gathered": (ip, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), pint, ip, pint,
+                                         ctypes.POINTER(ctypes.c_longlong)]),
+            "sift_multi_stats": (ip, [vp, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
+                                      ctypes.POINTER(ctypes.c_longlong)]),
+            "sift_multi_rccl_version": (ip, []),
+            "sift_multi_copy_gathered": (ip, [vp, vp, fp, ip, pint]),
         }
         optional = {"sift_graph_stats"}  # absent from older builds (A/B runs against a saved library)
         for name, (res, args) in sigs.items():
@@ -353,6 +367,127 @@ class Context:
                     self._L.sift_get_stage_stats(self.h, buf, 32, ctypes.byref(n), int(reset)))
         return {buf[i].name.decode(): dict(launches=buf[i].launches, ms=buf[i].ms, flops=buf[i].flops,
                                            bytes=buf[i].bytes) for i in range(n.value)}
+
+
+def multi_shard(batch: int, n_devices: int, index: int) -> tuple[int, int]:
+    """(first, count) of device `index`'s contiguous shard (sift_multi_shard)."""
+    f, c = ctypes.c_int(0), ctypes.c_int(0)
+    rc = lib().sift_multi_shard(batch, n_devices, index, ctypes.byref(f), ctypes.byref(c))
+    if rc != SIFT_OK:
+        raise SiftError("sift_multi_shard", rc, "bad arguments")
+    return f.value, c.value
+
+
+def multi_merge_offsets(shard_offsets) -> np.ndarray:
+    """Global per-image offsets from each shard's own (sift_multi_merge_offsets)."""
+    arrs = [np.ascontiguousarray(o, np.int32) for o in shard_offsets]
+    pint = ctypes.POINTER(ctypes.c_int)
+    ptrs = (pint * len(arrs))(*[a.ctypes.data_as(pint) for a in arrs])
+    counts = np.array([len(a) - 1 for a in arrs], np.int32)
+    out = np.zeros(int(counts.sum()) + 1, np.int32)
+    rc = lib().sift_multi_merge_offsets(ptrs, counts.ctypes.data_as(pint), len(arrs), out.ctypes.data_as(pint))
+    if rc != SIFT_OK:
+        raise SiftError("sift_multi_merge_offsets", rc, "bad arguments")
+    return out
+
+
+class MultiContext:
+    """Multi-GPU batch mode (sift_multi_*): one context + stream per device,
+    contiguous image shards, the keypoint records (and optionally the
+    descriptors) gathered to devices[0] over RCCL one step behind."""
+
+    def __init__(self, devices, max_rows: int, max_cols: int, max_batch_per_device: int, kp_cap_per_device: int,
+                 flags: int = 0, gather_desc: bool = False):
+        self._L = lib()
+        self.devices = list(devices)
+        dv = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        rc = self._L.sift_multi_create(dv, len(self.devices), max_rows, max_cols, max_batch_per_device, flags,
+                                       kp_cap_per_device, int(gather_desc), ctypes.byref(h))
+        if rc != SIFT_OK:
+            raise SiftError("sift_multi_create", rc, "could not create the multi-GPU context (see stderr)")
+        self.h = h
+        self.gather_desc = gather_desc
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.sift_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, fn, rc):
+        if rc != SIFT_OK:
+            raise SiftError(fn, rc, self._L.sift_multi_last_error(self.h).decode())
+
+    def context_handle(self, index: int):
+        return self._L.sift_multi_context(self.h, index)
+
+    def set_octaves(self, n: int):
+        for i in range(len(self.devices)):
+            rc = self._L.sift_set_octaves(ctypes.c_void_p(self.context_handle(i)), n)
+            self._check("sift_set_octaves", rc)
+
+    def synth_images(self, index: int, out_ptr: int, batch: int, rows: int, cols: int, row_stride: int,
+                     img_stride: int, seed_base: int = 0):
+        rc = self._L.sift_synth_images(ctypes.c_void_p(self.context_handle(index)), ctypes.c_void_p(out_ptr), batch,
+                                       rows, cols, row_stride, img_stride, seed_base)
+        self._check("sift_synth_images", rc)
+
+    def step(self, img_ptrs, counts, rows: int, cols: int, row_stride: int, img_stride: int):
+        n = len(self.devices)
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.c_void_p(p) for p in img_ptrs])
+        cnt = (ctypes.c_int * n)(*counts)
+        self._check("sift_multi_step", self._L.sift_multi_step(self.h, ptrs, cnt, rows, cols, row_stride, img_stride))
+
+    def flush(self):
+        self._check("sift_multi_flush", self._L.sift_multi_flush(self.h))
+
+    def gathered(self, offsets_cap: int):
+        """(device pointer to the records, to the descriptors or None, global
+        offsets as numpy, step index) of the last gathered step."""
+        k, d = ctypes.c_void_p(), ctypes.c_void_p()
+        offs = np.zeros(offsets_cap, np.int32)
+        bt, st = ctypes.c_int(0), ctypes.c_longlong(0)
+        self._check("sift_multi_gathered",
+                    self._L.sift_multi_gathered(self.h, ctypes.byref(k), ctypes.byref(d),
+                                                offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), offsets_cap,
+                                                ctypes.byref(bt), ctypes.byref(st)))
+        return k.value, d.value, offs[:bt.value + 1].copy(), st.value
+
+    def copy_gathered(self):
+        """Host copies (keypoints, descriptors or None) of the last gathered step."""
+        n = ctypes.c_int(0)
+        rc = self._L.sift_multi_copy_gathered(self.h, None, None, 0, ctypes.byref(n))
+        if rc not in (SIFT_OK, SIFT_E_CAPACITY):
+            self._check("sift_multi_copy_gathered", rc)
+        kps = np.zeros(n.value, KEYPOINT_DTYPE)
+        desc = np.zeros((n.value, DESC_LEN), np.float32) if self.gather_desc else None
+        if n.value:
+            self._check("sift_multi_copy_gathered",
+                        self._L.sift_multi_copy_gathered(self.h, kps.ctypes.data,
+                                                         _fp(desc) if desc is not None else None, n.value,
+                                                         ctypes.byref(n)))
+        return kps, desc
+
+    def stats(self):
+        v = [ctypes.c_longlong(0) for _ in range(3)]
+        self._check("sift_multi_stats", self._L.sift_multi_stats(self.h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("steps", "records", "transfers"), (x.value for x in v)))
+
+
+def rccl_version() -> int:
+    return lib().sift_multi_rccl_version()
 
 
 # ---- module-level API with the reference's names (one shared context) -------

@@ -77,6 +77,21 @@ def test_main_shaped_caller_compiles_with_header_only(tmp_path, siftgpu, openmp)
     assert exe.exists()
 
 
+def build_multi_gpu_host(out_path):
+    """tests/cpp/multi_gpu.cpp: a C++ host driving configs[3] through the C
+    ABI's sift_multi_* (g++ + the HIP runtime API, no hipcc)."""
+    src = os.path.join(ROOT, "tests", "cpp", "multi_gpu.cpp")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROOT, "include"),
+                    "-I", "/opt/rocm/include", src, "-o", str(out_path), "-L", os.path.join(PKG, "lib"),
+                    "-lsift_hip", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{os.path.join(PKG, 'lib')}",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    return out_path
+
+
+def test_multi_gpu_host_compiles(tmp_path, siftgpu):
+    assert build_multi_gpu_host(tmp_path / "multi_gpu").exists()
+
+
 def test_ctx_create_fails_cleanly_without_gpu(siftgpu):
     import torch
     if torch.cuda.device_count() > 0:

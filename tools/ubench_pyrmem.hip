@@ -28,6 +28,15 @@
 //  15 = 12 with non-temporal stores
 //  16 = 6 with four neighbouring 64-column strips per 1024-thread workgroup
 //     (four independent groups of four waves, one CU)
+//  17 = 6 with STRIP-MAJOR destination planes (round 6, VERDICT r5 #2a): each
+//     64-column strip's rows stored contiguously (x -> strip (x >> 6), y,
+//     x & 63; the next plane 0 likewise in its own 64-column strips), so every
+//     wave's stores form one linear stream; source = the row-major image
+//  18 = 17 with a strip-major source too (octaves > 0 read plane 0 of the
+//     octave, which would then be strip-major: three contiguous pieces per row)
+//  19 ROW BANDS (VERDICT r5 #2b): a workgroup owns a band of 40 rows of one
+//     image and walks them 8 per step, all 30 strips per step (inner loop),
+//     row-major destination: each step writes 8 full rows of every plane
 //   hipcc -O3 --offload-arch=gfx950 tools/ubench_pyrmem.hip -o tools/ubench_pyrmem && ./tools/ubench_pyrmem
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -52,32 +61,41 @@ __global__ __launch_bounds__(MODE == 16 ? 1024 : 256) void pyrmem_kernel(const f
   constexpr int STR = C / SW;
   __shared__ __attribute__((aligned(16))) float ring4[MODE == 16 ? 4 : 1][2][8][NDMA * 64];
   constexpr bool kXcd = MODE == 6 || MODE == 8 || MODE == 9 || MODE >= 10;
+  constexpr bool kSM = MODE == 17 || MODE == 18;  // strip-major destination
+  constexpr int kBand = 40;                       // mode 19: rows per workgroup
   const int nb = (int)gridDim.x;
   int item = kXcd ? (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   const int grp = MODE == 16 ? (int)(threadIdx.x >> 8) : 0;
   if (MODE == 16) item = __builtin_amdgcn_readfirstlane(item * 4 + grp);
   float(&ring)[2][8][NDMA * 64] = ring4[grp];
-  const int b = item / STR, x0 = (item % STR) * SW;
+  const int b = MODE == 19 ? item / (R / kBand) : item / STR;
+  const int band0 = MODE == 19 ? (item % (R / kBand)) * kBand : 0;
   const int wv = (threadIdx.x >> 6) & 3, lane = threadIdx.x & 63;
   const float* simg = src + b * PLANE;
   const Rsrc rs = mk(simg, PLANE * 4);
   float* img = planes + (long long)b * 5 * PLANE;
-  const int sr = lane >> 4, xg = x0 + 4 * (lane & 15);
+  const int sr = lane >> 4;
   float4 v = make_float4(lane, 1.f, 2.f, 3.f);
-  for (int s = 0; s < R / 8; ++s) {
-    const int Ys = 8 * s;
+  constexpr int NSTEP = MODE == 19 ? kBand / 8 * STRIPS : R / 8;
+  for (int s = 0; s < NSTEP; ++s) {
+    const int x0 = MODE == 19 ? (s % STRIPS) * 64 : (item % STR) * SW;
+    const int Ys = MODE == 19 ? band0 + 8 * (s / STRIPS) : 8 * s;
+    const int xg = x0 + 4 * (lane & 15);
     if (wv == 0 && MODE >= 1 && MODE != 5) {
       float* slot = &ring[s & 1][0][0];
       constexpr bool kHalo = !(MODE == 7 || MODE == 8);
       if constexpr (MODE == 1 || MODE == 4 || MODE >= 6) {
         for (int i = 0; i < 8; ++i) {
-          const unsigned so = (unsigned)((Ys + i) * C * 4);
+          const unsigned so = MODE == 18 ? 0u : (unsigned)((Ys + i) * C * 4);
           const unsigned l0 = __builtin_amdgcn_readfirstlane(
               (unsigned)(size_t)(const __attribute__((address_space(3))) float*)(slot + i * NDMA * 64));
 #pragma unroll
           for (int d = 0; d < (kHalo ? NDMA : NSUB); ++d) {
             const int c = x0 - (kHalo ? 24 : 0) + lane + 64 * d;
-            const unsigned vo = c >= 0 && c < C - 1 ? c * 4u : 0x7f000000u;
+            // mode 18: the source plane is strip-major too
+            const unsigned vo = !(c >= 0 && c < C - 1) ? 0x7f000000u
+                                : MODE == 18 ? (unsigned)(((c >> 6) * R * 64 + (Ys + i) * 64 + (c & 63)) * 4)
+                                             : c * 4u;
             if (!kHalo || 64 * d + lane < SROW)
               asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, %3 offen lds" ::"s"(l0 + 256 * d), "v"(vo),
                            "s"(rs), "s"(so) : "memory", "m0");
@@ -110,14 +128,19 @@ __global__ __launch_bounds__(MODE == 16 ? 1024 : 256) void pyrmem_kernel(const f
       const int pa = wv == 0 ? 0 : wv == 1 ? 4 : wv == 2 ? 3 : 2;
       for (int r4 = 0; r4 < 8 * NSUB; r4 += 4) {
         const int y = Ys + (r4 & 7) + sr;
-        const unsigned off = (unsigned)(y * C + xg + 64 * (r4 >> 3)) * 4u;
+        const int xw = xg + 64 * (r4 >> 3);
+        const unsigned off = kSM ? (unsigned)((xw >> 6) * R * 64 + y * 64 + (xw & 63)) * 4u
+                                 : (unsigned)(y * C + xw) * 4u;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), mk(img + pa * PLANE, PLANE * 4),
                                                (int)off, 0, 0);
         if (wv == 3) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), mk(img + 1 * PLANE, PLANE * 4),
                                                  (int)off, 0, 0);
           const bool dn = (y & 1) == 0;
-          const unsigned offn = dn ? (unsigned)((y >> 1) * (C / 2) + ((xg + 64 * (r4 >> 3)) >> 1)) * 4u : 0x7f000000u;
+          const int xn = xw >> 1;  // next plane: R / 2 rows, C / 2 columns
+          const unsigned offn = !dn ? 0x7f000000u
+                                : kSM ? (unsigned)((xn >> 6) * (R / 2) * 64 + (y >> 1) * 64 + (xn & 63)) * 4u
+                                      : (unsigned)((y >> 1) * (C / 2) + xn) * 4u;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(v.x, v.z)),
                                                 mk(nxt + b * (PLANE / 4), PLANE), (int)offn, 0, 0);
         }
@@ -166,16 +189,17 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  const char* names[17] = {"stores_only", "stores+dma_dword", "stores+dma_dwordx4", "stores+load_dwordx4+ds_write",
+  const char* names[20] = {"stores_only", "stores+dma_dword", "stores+dma_dwordx4", "stores+load_dwordx4+ds_write",
                            "dma_dword_only", "stores_4waves", "stores+dma_dword_xcd", "stores+dma_dword_nohalo",
                            "stores+dma_dword_nohalo_xcd", "1plane+dma_dword_xcd", "strip128+dma_xcd", "strip256+dma_xcd",
                            "linear_streams", "linear_copy", "linear_writes_only", "linear_streams_nt",
-                           "4strips_per_wg+dma_xcd"};
-  for (int mode = 0; mode < 17; ++mode) {
+                           "4strips_per_wg+dma_xcd", "strip_major_dst+dma_xcd", "strip_major_dst+strip_major_src_xcd",
+                           "row_bands40+dma_xcd"};
+  for (int mode = 0; mode < 20; ++mode) {
     float best = 1e9f;
     for (int rep = 0; rep < 5; ++rep) {
       (void)hipEventRecord(e0);
-      const dim3 g(B * (mode == 10 ? C / 128 : mode == 11 || mode == 16 ? C / 256 : STRIPS)),
+      const dim3 g(B * (mode == 10 ? C / 128 : mode == 11 || mode == 16 ? C / 256 : mode == 19 ? R / 40 : STRIPS)),
           blk(mode == 16 ? 1024 : 256);
       switch (mode) {
         case 0: hipLaunchKernelGGL(pyrmem_kernel<0>, g, blk, 0, 0, src, planes, nxt); break;
@@ -194,6 +218,9 @@ int main() {
                              (float4*)nxt, (long long)B * PLANE / 4);
           break;
         case 16: hipLaunchKernelGGL(pyrmem_kernel<16>, g, blk, 0, 0, src, planes, nxt); break;
+        case 17: hipLaunchKernelGGL(pyrmem_kernel<17>, g, blk, 0, 0, src, planes, nxt); break;
+        case 18: hipLaunchKernelGGL(pyrmem_kernel<18>, g, blk, 0, 0, src, planes, nxt); break;
+        case 19: hipLaunchKernelGGL(pyrmem_kernel<19>, g, blk, 0, 0, src, planes, nxt); break;
         case 13:
           hipLaunchKernelGGL(linear_mix_kernel<1>, dim3((unsigned)((long long)B * PLANE / 4 / 1024)), blk, 0, 0, (const float4*)src, (float4*)planes,
                              (float4*)nxt, (long long)B * PLANE / 4);
