@@ -91,16 +91,17 @@ __device__ __forceinline__ void slab(float a, float inv_a, float b, int& lo, int
   hi = min(hi, (int)fminf(floorf(x1), 1e6f));
 }
 
-// Record hand-off (packed, round 2): values at [group][owner][sample] (2 KB,
-// XOR-swizzled so the owner's two ds_read_b128 are conflict free and each
-// store address is one XOR), the bin bytes handed to their owners in
+// Record hand-off (packed, round 2): values in a 2 KB array laid out so that
+// the eight ds_write_b32 of a batch are bank-conflict free whatever the
+// samples' parities (round 6, see the store), each store address one XOR, the
+// owner's two ds_read_b128 at most 2-way; the bin bytes handed to their owners in
 // registers (round 4), a 16-bit row table for caller keypoints (1.3 KB; DET:
 // 32-bit cumulative entries, 2.7 KB), and the in-flight records packed as 8
 // values + 2 words of bin bytes, so four waves per SIMD fit.  (Round 1's
 // float2 (qidx, value) records at [sample][group][owner] with a trash row,
 // 12.4 KB per wave and three waves per SIMD, were 8.71 vs 8.39 ms per step:
 // tools/patches/r5_variants.patch.)
-constexpr int kRecG = 64;  // value words per group (8 owners x 8 samples, XOR-swizzled, see the store)
+constexpr int kRecG = 64;  // value words per group (8 owners x 8 samples, see the store)
 
 struct RecT {  // one lane's 8 corner records
   float v[8];
@@ -447,10 +448,10 @@ descriptor_kernel(DescArgs A) {
         out.qb[1] = __builtin_amdgcn_perm(0x00000a0au, 0x0a000000u, selR1) + c4;
       }
       // the slot bits of the hand-off store address from the parities of X =
-      // Rm + 1 and Y = Cm + 1 -- (odd ^ 6) << 5, i.e. slot s is stored at
+      // Rm + 1 and Y = Cm + 1 -- (odd ^ 6) << 7, i.e. slot s is stored at
       // position s ^ 6 (the owner reads there) -- by shift-and-or steps
       (void)odd;
-      odd_out = ((X << 7) & 0x80) | ((Y << 6) & 0x40) | ((O0 & 1) << 5);
+      odd_out = ((X << 9) & 0x200) | ((Y << 8) & 0x100) | ((O0 & 1) << 7);
     };
     auto sample = [&](bool in_range, RecT& out, int& odd_out) {
       Loc L;
@@ -521,20 +522,25 @@ descriptor_kernel(DescArgs A) {
     // located in this step
     auto step = [&](int base, Loc& ln, Loc& l2) {
       {
-        // corner k to owner slot s = k ^ odd: value at byte (g << 8) | ((s ^ 6) << 5) |
-        // (q << 2), bit 4 flipped on odd groups (so a 16-lane pass of the
-        // owners' ds_read_b128 -- an even and an odd group -- covers all 64
-        // banks); bin byte at (g << 6) | (s << 3) | q.  Slot bits are clear
-        // in both bases, so each address is one XOR with k's slot bits.
-        // (Round 3 measured a layout whose stores are at most 2-way
-        // conflicted -- value at (32g + 4q) ^ TB(s), TB XOR-linear in s, reads
-        // still conflict free: SQ_LDS_BANK_CONFLICT -35 %, but the slot
-        // swizzle costs ~3 VALU per batch and the kernel took 7.57-7.69 vs
-        // 7.45-7.47 ms: it is bound by VALU issue, not by the conflicts.)
+        // corner k to owner slot s = k ^ odd: value at byte
+        //   ((g >> 2) << 10) | ((s ^ 6) << 7) | ((g & 3) << 5) | (q << 2).
+        // A ds_write_b32 banks on (a / 4) mod 32 per 32-lane half (MI355X:
+        // LDS table), i.e. on byte bits 2-6 = (q, g & 3): one store
+        // instruction's 64 lanes hit 32 distinct banks per half whatever the
+        // data-dependent slots -- conflict free.  (Round 2-5's layout, with the
+        // slot bits at 5-7, left two of them in the store's bank and put 4
+        // lanes of random slots on each bank column: 47.4 instead of 16
+        // LDS-array cycles per batch's eight stores, simulated; the 0.34 of
+        // SQ_LDS_IDX_ACTIVE that SQ_LDS_BANK_CONFLICT measured.)  The owner's
+        // ds_read_b128 (16-lane groups, (a / 4) mod 64) see bits 4-7 = (half,
+        // g & 3, s & 1): 2-way, 16 instead of 8 cycles per batch.  No layout
+        // makes both conflict free: data-independent store banks leave the
+        // reads only bit 7 for the slot.  Slot bits are clear in the base, so
+        // each store address is one XOR with k's slot bits, as before.
         char* rb = reinterpret_cast<char*>(rec);
-        const int wv = ((g << 8) | ((q << 2) ^ ((g & 1) << 4))) | odd_cur;  // odd_cur = odd << 5
+        const int wv = (((g >> 2) << 10) | ((g & 3) << 5) | (q << 2)) | odd_cur;  // odd_cur = (odd ^ 6) << 7
 #pragma unroll
-        for (int k = 0; k < 8; ++k) *reinterpret_cast<float*>(rb + (wv ^ (k << 5))) = rc_cur.v[k];
+        for (int k = 0; k < 8; ++k) *reinterpret_cast<float*>(rb + (wv ^ (k << 7))) = rc_cur.v[k];
         // bin bytes to their owners in registers (round 4; were eight
         // ds_write_b8 per lane and one ds_read_b64): byte s of this lane's
         // pair is corner s ^ odd's (finish), then an 8 x 8 byte transpose over the group's
@@ -572,9 +578,10 @@ descriptor_kernel(DescArgs A) {
       // ordered accumulation of batch k: lane q applies its record of each sample
       {
         const char* rb = reinterpret_cast<const char*>(rec);
-        const int rv = (g << 8) | ((q ^ 6) << 5);  // slot q at position q ^ 6 (finish's odd_out)  // samples 0-3 at bit 4 = g & 1, samples 4-7 at the other half
-        const float4 va = *reinterpret_cast<const float4*>(rb + (rv | ((g & 1) << 4)));
-        const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | (((g & 1) ^ 1) << 4)));
+        // slot q at position q ^ 6 (finish's odd_out); samples 0-3, then 4-7 (bit 4)
+        const int rv = ((g >> 2) << 10) | ((q ^ 6) << 7) | ((g & 3) << 5);
+        const float4 va = *reinterpret_cast<const float4*>(rb + rv);
+        const float4 vb = *reinterpret_cast<const float4*>(rb + (rv | 16));
         const uint2 qq = qq_cur;
         const float vals[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
         // byte address qidx * 256 + lane * 4 in one v_perm_b32: byte 0 <- lane * 4

@@ -24,5 +24,5 @@ for f in $W/sift-gpu_amd/csrc/*.hip; do
   OBJS="$OBJS $o"
 done
 for p in $pids; do wait $p; done
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/libsift_hip_$NAME.so $OBJS
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/libsift_hip_$NAME.so $OBJS -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built lib/libsift_hip_$NAME.so from $2"

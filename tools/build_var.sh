@@ -12,7 +12,8 @@ OBJS=$(ls build/*.o | grep -v "/$base.o")
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   /opt/rocm/bin/hipcc $F $defs -c csrc/$SRC -o build/var_$name.o.tmp 2>/dev/null
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/libsift_hip_$name.so $OBJS build/var_$name.o.tmp
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/libsift_hip_$name.so $OBJS build/var_$name.o.tmp \
+    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
   rm build/var_$name.o.tmp
   echo "built lib/libsift_hip_$name.so ($defs)"
 done
