@@ -79,7 +79,8 @@ def parse():
     p.add_argument("--streams", type=int, default=2,
                    help="timed legs: the per-GPU batch as this many sub-batches, one context + HIP stream each")
     p.add_argument("--no-8k", action="store_true", help="skip the configs[4] 7680x4320 leg")
-    p.add_argument("--only", default=None, choices=[None, "exact", "fast", "single", "8k"],
+    p.add_argument("--no-multi", action="store_true", help="skip the C-ABI multi-GPU (sift_multi_*) leg")
+    p.add_argument("--only", default=None, choices=[None, "exact", "fast", "single", "8k", "multi"],
                    help="profiling runs: time only this leg")
     p.add_argument("--profile-json", default=None, help="also write per-stage stats here")
     return p.parse_args()
@@ -408,6 +409,39 @@ def eightk_leg(steps, warmup, R8=4320, C8=7680):
                 "note": "latency = median wall time of sift_detect_compute_batch(batch 1) + sift_sync, image "
                         "resident in HBM (graph replay); roofline legs use PROFILE-mode HIP events per stage"})
     return out
+
+
+# ---- the C-ABI multi-GPU path (sift_multi_*, csrc/multi.hip) at n = 1 ----------
+def c_abi_multi_leg(env, steps, warmup):
+    """configs[3]'s C++-host path on this GPU alone: the headline batch
+    (--batch images, this rank's synthetic images) through sift_multi_step on
+    one device -- one context, graph replay, the records gathered one step
+    behind by RCCL's self send/recv -- timed like a leg (flush inside the
+    timed region).  The rate beside `value` shows what the C ABI's multi path
+    costs against bench.py's two-stream Python driver."""
+    a = env.a
+    B, R, C = env.B, env.R, env.C
+    with siftgpu.MultiContext([env.dev], R, C, B, B * 40000) as m:
+        m.set_octaves(env.octaves)
+        ptr = env.imgs.data_ptr()
+        for _ in range(warmup):
+            m.step([ptr], [B], R, C, C, R * C)
+        m.flush()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m.step([ptr], [B], R, C, C, R * C)
+        m.flush()
+        dt = time.perf_counter() - t0
+        _, _, offs, _ = m.gathered(B + 1)
+        st = m.stats()
+    return {"n_devices": 1, "Mpix_per_s": round(B * R * C * steps / 1e6 / dt, 2),
+            "ms_per_step": round(dt / steps * 1e3, 3), "keypoints_per_step": int(offs[-1]),
+            "rccl_version": siftgpu.rccl_version(), "p2p_transfers": st["transfers"],
+            "records_gathered": st["records"],
+            "note": "sift_multi_create/_step/_flush (include/sift_hip.h) on this one GPU: one context and "
+                    "stream (no two-stream overlap), the 28-B records gathered to device 0 one step behind "
+                    "over RCCL (self send/recv at n = 1); tests/cpp/multi_gpu.cpp is the same path from C++"}
 
 
 # ---- knnMatch leg (SURVEY 8(f) f2) ---------------------------------------------
@@ -855,6 +889,8 @@ def assemble(a, world, env_shape, res, cpu, errors):
         out["single_image"] = res["single"]
     if res.get("eightk") is not None:
         out["image_8k"] = res["eightk"]
+    if res.get("multi") is not None:
+        out["c_abi_multi"] = res["multi"]
     if cpu:
         out.update(cpu)
         cb = cpu.get("cpu_baseline")
@@ -866,7 +902,7 @@ def assemble(a, world, env_shape, res, cpu, errors):
                 res["single"]["keypoints_per_s"] / cb["keypoints_per_s"], 1)
     for name in errors:
         block = {"fast": "fast_mode", "fast_block": "fast_mode", "match": "match", "match_block": "match",
-                 "single": "single_image", "eightk": "image_8k"}.get(name)
+                 "single": "single_image", "eightk": "image_8k", "multi": "c_abi_multi"}.get(name)
         if block and block not in out:
             out[block] = {"error": errors[name]}
     if errors:
@@ -1016,6 +1052,8 @@ def main():
         res["single"] = guarded(errors, "single", single_image_leg, env.R, env.C, a.steps, a.warmup)
     if rank == 0 and world == 1 and not a.no_8k and want("8k"):
         res["eightk"] = guarded(errors, "eightk", eightk_leg, a.steps, a.warmup)
+    if rank == 0 and world == 1 and not a.no_multi and want("multi"):
+        res["multi"] = guarded(errors, "multi", c_abi_multi_leg, env, a.steps, a.warmup)
     verified_ok = True
     if rank == 0:
         out = assemble(a, world, (env.B, env.R, env.C, env.S), res, cpu, errors)

@@ -58,20 +58,21 @@ def test_line_survives_failing_legs(bench, monkeypatch, capsys):
     monkeypatch.setattr(bench, "run_match", boom)
     monkeypatch.setattr(bench, "single_image_leg", boom)
     monkeypatch.setattr(bench, "eightk_leg", boom)
+    monkeypatch.setattr(bench, "c_abi_multi_leg", boom)
     out = _run(bench, monkeypatch, capsys, [])
     assert out["value"] > 0 and out["unit"] == "Mpix/s" and out["n_gpus"] == 1
     assert out["roofline"]["kernel"] == "blur_sym_kernel" and out["roofline"]["frac"] > 0
     assert out["cpu_baseline"]["value"] == 0.6 and "speedup_vs_cpu_1thread" in out
-    for block in ("fast_mode", "match", "single_image", "image_8k"):
+    for block in ("fast_mode", "match", "single_image", "image_8k", "c_abi_multi"):
         assert "leg exploded" in out[block]["error"]
-    assert set(out["leg_errors"]) == {"fast", "match", "single", "eightk"}
+    assert set(out["leg_errors"]) == {"fast", "match", "single", "eightk", "multi"}
 
 
 def test_line_survives_failing_cpu_leg(bench, monkeypatch, capsys):
     def boom(*a, **k):
         raise TimeoutError("cpu leg hung")
     monkeypatch.setattr(bench, "cpu_baseline_parallel", boom)
-    for leg in ("run_fast", "run_match", "single_image_leg", "eightk_leg"):
+    for leg in ("run_fast", "run_match", "single_image_leg", "eightk_leg", "c_abi_multi_leg"):
         monkeypatch.setattr(bench, leg, lambda *a, **k: None)
     out = _run(bench, monkeypatch, capsys, [])
     assert out["value"] > 0 and out["cpu_baseline"]["value"] == 0.6
@@ -79,7 +80,7 @@ def test_line_survives_failing_cpu_leg(bench, monkeypatch, capsys):
 
 
 def _quiet_legs(B, monkeypatch):
-    for leg in ("run_fast", "run_match", "single_image_leg", "eightk_leg"):
+    for leg in ("run_fast", "run_match", "single_image_leg", "eightk_leg", "c_abi_multi_leg"):
         monkeypatch.setattr(B, leg, lambda *a, **k: None)
 
 
@@ -215,7 +216,7 @@ def test_gpu_error_flag_by_exception_type(bench, monkeypatch, capsys):
 def test_line_survives_failing_block(bench, monkeypatch, capsys):
     """A leg that returns but whose block cannot be built (missing stage)."""
     monkeypatch.setattr(bench, "run_fast", lambda env: ((0.05, {}, 1.0), None))
-    for leg in ("run_match", "single_image_leg", "eightk_leg"):
+    for leg in ("run_match", "single_image_leg", "eightk_leg", "c_abi_multi_leg"):
         monkeypatch.setattr(bench, leg, lambda *a, **k: None)
     out = _run(bench, monkeypatch, capsys, ["--no-cpu-baseline"])
     assert out["value"] > 0 and "error" in out["fast_mode"]
