@@ -415,13 +415,13 @@ def eightk_leg(steps, warmup, R8=4320, C8=7680):
 def c_abi_multi_leg(env, steps, warmup):
     """configs[3]'s C++-host path on this GPU alone: the headline batch
     (--batch images, this rank's synthetic images) through sift_multi_step on
-    one device -- one context, graph replay, the records gathered one step
-    behind by RCCL's self send/recv -- timed like a leg (flush inside the
-    timed region).  The rate beside `value` shows what the C ABI's multi path
+    one device -- --streams contexts and HIP streams as in the headline, graph
+    replay, the records gathered one step behind by RCCL's self send/recv --
+    timed like a leg (flush inside the timed region).  The rate beside `value` shows what the C ABI's multi path
     costs against bench.py's two-stream Python driver."""
     a = env.a
     B, R, C = env.B, env.R, env.C
-    with siftgpu.MultiContext([env.dev], R, C, B, B * 40000) as m:
+    with siftgpu.MultiContext([env.dev], R, C, B, B * 40000, streams_per_device=env.S) as m:
         m.set_octaves(env.octaves)
         ptr = env.imgs.data_ptr()
         for _ in range(warmup):
@@ -435,13 +435,14 @@ def c_abi_multi_leg(env, steps, warmup):
         dt = time.perf_counter() - t0
         _, _, offs, _ = m.gathered(B + 1)
         st = m.stats()
-    return {"n_devices": 1, "Mpix_per_s": round(B * R * C * steps / 1e6 / dt, 2),
+    return {"n_devices": 1, "streams_per_device": env.S, "Mpix_per_s": round(B * R * C * steps / 1e6 / dt, 2),
             "ms_per_step": round(dt / steps * 1e3, 3), "keypoints_per_step": int(offs[-1]),
             "rccl_version": siftgpu.rccl_version(), "p2p_transfers": st["transfers"],
             "records_gathered": st["records"],
-            "note": "sift_multi_create/_step/_flush (include/sift_hip.h) on this one GPU: one context and "
-                    "stream (no two-stream overlap), the 28-B records gathered to device 0 one step behind "
-                    "over RCCL (self send/recv at n = 1); tests/cpp/multi_gpu.cpp is the same path from C++"}
+            "note": "sift_multi_create/_step/_flush (include/sift_hip.h) on this one GPU: the shard as "
+                    "streams_per_device sub-batches on their own contexts and HIP streams, the 28-B records "
+                    "gathered to device 0 one step behind over RCCL (self send/recv at n = 1); "
+                    "tests/cpp/multi_gpu.cpp is the same path from C++"}
 
 
 # ---- knnMatch leg ---------------------------------------------

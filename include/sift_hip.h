@@ -154,20 +154,29 @@ int sift_multi_shard(int batch, int n_devices, int index, int* first, int* count
  * [counts[i] + 1] (records concatenated in device order).  No GPU needed. */
 int sift_multi_merge_offsets(const int* const* shard_offsets, const int* counts, int n_devices,
                              int* global_offsets);
-/* One sift_ctx (own HIP stream) per device, two result slots of
- * kp_cap_per_device records per device, a gather stream per device, the
- * gather buffers on devices[0] (n_devices x kp_cap_per_device records, and
- * descriptors when gather_desc), and RCCL communicators over the devices.
- * Device indices must be distinct (RCCL: one rank per device). */
+/* Per device: streams_per_device sift_ctx contexts, each with its own HIP
+ * stream (0 = the default, 2: each step's shard runs as that many contiguous
+ * sub-batches whose stages overlap, as bench.py's streams do), two result
+ * slots per context sharing kp_cap_per_device records per slot, and a
+ * gather stream; on devices[0] the gather buffers (n_devices x
+ * kp_cap_per_device records, and descriptors when gather_desc); RCCL
+ * communicators over the devices.  Device indices must be distinct (RCCL:
+ * one rank per device). */
 int sift_multi_create(const int* devices, int n_devices, int max_rows, int max_cols, int max_batch_per_device,
-                      unsigned flags, int kp_cap_per_device, int gather_desc, sift_multi** out);
+                      unsigned flags, int streams_per_device, int kp_cap_per_device, int gather_desc,
+                      sift_multi** out);
 int sift_multi_destroy(sift_multi* m);
 const char* sift_multi_last_error(const sift_multi* m);
-/* The context of device index i (flags, octaves, sift_synth_images, ...). */
+/* The first context of device index i (sift_synth_images on that device, ...). */
 sift_ctx* sift_multi_context(sift_multi* m, int index);
+/* sift_set_octaves / sift_set_flags on every context. */
+int sift_multi_set_octaves(sift_multi* m, int n_octaves);
+int sift_multi_set_flags(sift_multi* m, unsigned flags);
 /* One step: device i detects + describes counts[i] images resident on it
  * (d_imgs[i], strides in elements as in sift_detect_compute_batch) into its
- * result slot, and the previous step's records are gathered to devices[0].
+ * result slots, and the previous step's records are gathered to devices[0].
+ * The images must be complete when the step is enqueued (the contexts'
+ * streams do not wait for the caller's producers: synchronise them first).
  * Asynchronous, except that the host waits for the previous step's per-image
  * offsets (one step behind, so normally without blocking). */
 int sift_multi_step(sift_multi* m, const float* const* d_imgs, const int* counts, int rows, int cols,

@@ -8,10 +8,13 @@
 // behind the compute so it overlaps it:
 //
 //   step k (slot s = k & 1):
-//     every device i: its context stream waits until the gather of step k - 2
-//       has read slot s, runs sift_detect_compute_batch on its shard into
-//       slot s (graph replay), copies the shard's per-image offsets to pinned
-//       host memory and records cdone[i][s];
+//     every device i runs its shard as S contiguous sub-batches, one context
+//     and HIP stream each (bench.py's two-stream overlap: the sub-batches'
+//     VALU-bound blur and latency-bound descriptor phases run beside each
+//     other); each sub-batch's stream waits until the gather of step k - 2
+//     has read slot s, runs sift_detect_compute_batch into slot s (graph
+//     replay), copies its per-image offsets to pinned host memory and records
+//     cdone[unit][s];
 //     then the gather of step k - 1 (slot p = s ^ 1): the host waits for
 //       cdone[*][p] (normally complete: step k is queued behind it), reads the
 //       record counts, and one ncclGroupStart / ncclGroupEnd posts, on a
@@ -23,8 +26,9 @@
 //   flush: the gather of the last step, then every stream is drained and the
 //     contexts' sticky status reported.
 //
-// One process, one HIP context + stream per device (sift_ctx), communicators
-// from ncclCommInitAll (RCCL over xGMI).  Layered on the public C ABI only.
+// One process, S contexts + HIP streams per device (sift_ctx; a "unit" is one
+// of them), a gather stream per device, communicators from ncclCommInitAll
+// (RCCL over xGMI).  Layered on the public C ABI only.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -35,21 +39,23 @@
 #include "../../include/sift_hip.h"
 
 struct sift_multi {
-  int n = 0;
+  int n = 0;   // devices
+  int S = 1;   // contexts (sub-batches, streams) per device; unit u = i * S + j
   std::vector<int> dev;
-  std::vector<sift_ctx*> ctx;
-  std::vector<ncclComm_t> comm;
+  std::vector<sift_ctx*> ctx;                         // per unit
+  std::vector<ncclComm_t> comm;                       // per device
   std::vector<hipStream_t> gstream;                   // per device: the gather stream
-  std::vector<hipEvent_t> cdone[2], gdone[2];         // per slot, per device
-  std::vector<sift_keypoint*> kbuf[2];                // per slot, per device: kp_cap records
-  std::vector<float*> dbuf[2];                        // per slot, per device: kp_cap x 128
-  std::vector<int*> doff[2];                          // per slot, per device: [max_batch + 1]
+  std::vector<hipEvent_t> gdone[2];                   // per slot, per device: slot free again
+  std::vector<hipEvent_t> cdone[2];                   // per slot, per unit: compute done
+  std::vector<sift_keypoint*> kbuf[2];                // per slot, per unit: cap records
+  std::vector<float*> dbuf[2];                        // per slot, per unit: cap x 128
+  std::vector<int*> doff[2];                          // per slot, per unit: [max_batch + 1]
   std::vector<int*> hoff[2];                          // pinned copies of doff
-  std::vector<int> cnt[2];                            // per slot: images of each device's shard
-  sift_keypoint* rk = nullptr;                        // device 0: gathered records, n x kp_cap
+  std::vector<int> cnt[2];                            // per slot, per unit: images of the sub-batch
+  sift_keypoint* rk = nullptr;                        // device 0: gathered records, U x cap
   float* rd = nullptr;                                // device 0: gathered descriptors (gather_desc)
   std::vector<int> goff;                              // host: global offsets of the last gather
-  int max_batch = 0, kp_cap = 0, gather_desc = 0;
+  int max_batch = 0, cap = 0, gather_desc = 0;        // cap: records per unit and slot
   long long steps = 0;       // steps enqueued
   long long gathered = -1;   // step index held by rk / goff (-1: none)
   bool pending = false;      // the last enqueued step is not gathered yet
@@ -80,44 +86,47 @@ int mfail(sift_multi* m, int code, const std::string& msg) {
 
 // Gathers slot p (the step whose per-image offsets are in hoff[p]) to device 0.
 int gather_slot(sift_multi* m, int p) {
-  const int n = m->n;
-  std::vector<long long> nrec(n);
+  const int U = m->n * m->S;
+  std::vector<long long> nrec(U);
   long long total = 0;
-  for (int i = 0; i < n; ++i) {
-    MHIP(m, hipSetDevice(m->dev[i]));
-    MHIP(m, hipEventSynchronize(m->cdone[p][i]));  // one step behind: normally already complete
-    const int c = m->cnt[p][i];
-    const long long k = c > 0 ? m->hoff[p][i][c] : 0;
-    if (k > m->kp_cap)
-      return mfail(m, SIFT_E_CAPACITY, "device " + std::to_string(m->dev[i]) + ": " + std::to_string(k) +
-                                           " keypoints exceed kp_cap_per_device " + std::to_string(m->kp_cap));
-    nrec[i] = k;
+  for (int u = 0; u < U; ++u) {
+    MHIP(m, hipSetDevice(m->dev[u / m->S]));
+    MHIP(m, hipEventSynchronize(m->cdone[p][u]));  // one step behind: normally already complete
+    const int c = m->cnt[p][u];
+    const long long k = c > 0 ? m->hoff[p][u][c] : 0;
+    if (k > m->cap)
+      return mfail(m, SIFT_E_CAPACITY, "device " + std::to_string(m->dev[u / m->S]) + ": " + std::to_string(k) +
+                                           " keypoints in a sub-batch exceed its share of kp_cap_per_device (" +
+                                           std::to_string(m->cap) + ")");
+    nrec[u] = k;
     total += k;
   }
-  // global per-image offsets (contiguous shards: device order = image order)
+  // global per-image offsets (contiguous shards and sub-batches: unit order = image order)
   int batch_total = 0;
-  for (int i = 0; i < n; ++i) batch_total += m->cnt[p][i];
+  for (int u = 0; u < U; ++u) batch_total += m->cnt[p][u];
   m->goff.assign(batch_total + 1, 0);
   std::vector<const int*> so(m->hoff[p].begin(), m->hoff[p].end());
-  (void)sift_multi_merge_offsets(so.data(), m->cnt[p].data(), n, m->goff.data());
-  for (int i = 0; i < n; ++i) {
-    MHIP(m, hipSetDevice(m->dev[i]));
-    MHIP(m, hipStreamWaitEvent(m->gstream[i], m->cdone[p][i], 0));
+  (void)sift_multi_merge_offsets(so.data(), m->cnt[p].data(), U, m->goff.data());
+  for (int u = 0; u < U; ++u) {
+    MHIP(m, hipSetDevice(m->dev[u / m->S]));
+    MHIP(m, hipStreamWaitEvent(m->gstream[u / m->S], m->cdone[p][u], 0));
   }
   MNCCL(m, ncclGroupStart());
   long long at = 0;
-  for (int i = 0; i < n; ++i) {
-    if (nrec[i] > 0) {
-      // device i sends, device 0 receives at the record offset of shard i
-      // (device 0 to itself as well: one code path, RCCL's self p2p)
-      ncclResult_t r = ncclSend(m->kbuf[p][i], (size_t)nrec[i] * sizeof(sift_keypoint), ncclUint8, 0, m->comm[i],
+  for (int u = 0; u < U; ++u) {
+    const int i = u / m->S;
+    if (nrec[u] > 0) {
+      // device i sends, device 0 receives at the record offset of unit u
+      // (device 0 to itself as well: one code path, RCCL's self p2p); the
+      // pairs between two devices match in posting order
+      ncclResult_t r = ncclSend(m->kbuf[p][u], (size_t)nrec[u] * sizeof(sift_keypoint), ncclUint8, 0, m->comm[i],
                                 m->gstream[i]);
       if (r == ncclSuccess)
-        r = ncclRecv(m->rk + at, (size_t)nrec[i] * sizeof(sift_keypoint), ncclUint8, i, m->comm[0], m->gstream[0]);
+        r = ncclRecv(m->rk + at, (size_t)nrec[u] * sizeof(sift_keypoint), ncclUint8, i, m->comm[0], m->gstream[0]);
       if (r == ncclSuccess && m->gather_desc) {
-        r = ncclSend(m->dbuf[p][i], (size_t)nrec[i] * SIFT_DESC_LEN, ncclFloat32, 0, m->comm[i], m->gstream[i]);
+        r = ncclSend(m->dbuf[p][u], (size_t)nrec[u] * SIFT_DESC_LEN, ncclFloat32, 0, m->comm[i], m->gstream[i]);
         if (r == ncclSuccess)
-          r = ncclRecv(m->rd + at * SIFT_DESC_LEN, (size_t)nrec[i] * SIFT_DESC_LEN, ncclFloat32, i, m->comm[0],
+          r = ncclRecv(m->rd + at * SIFT_DESC_LEN, (size_t)nrec[u] * SIFT_DESC_LEN, ncclFloat32, i, m->comm[0],
                        m->gstream[0]);
       }
       if (r != ncclSuccess) {
@@ -126,10 +135,10 @@ int gather_slot(sift_multi* m, int p) {
       }
       m->transfers += m->gather_desc ? 2 : 1;
     }
-    at += nrec[i];
+    at += nrec[u];
   }
   MNCCL(m, ncclGroupEnd());
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < m->n; ++i) {
     MHIP(m, hipSetDevice(m->dev[i]));
     MHIP(m, hipEventRecord(m->gdone[p][i], m->gstream[i]));
   }
@@ -169,25 +178,35 @@ const char* sift_multi_last_error(const sift_multi* m) { return m ? m->err.c_str
 
 int sift_multi_destroy(sift_multi* m) {
   if (!m) return SIFT_OK;
-  for (int i = 0; i < m->n; ++i) {
-    (void)hipSetDevice(m->dev[i]);
-    if (i < (int)m->gstream.size() && m->gstream[i]) (void)hipStreamSynchronize(m->gstream[i]);
-    if (i < (int)m->ctx.size() && m->ctx[i]) (void)hipStreamSynchronize((hipStream_t)sift_get_stream(m->ctx[i]));
-  }
+  const int U = (int)m->ctx.size();
+  for (int u = 0; u < U; ++u)
+    if (m->ctx[u]) {
+      (void)hipSetDevice(m->dev[u / m->S]);
+      (void)hipStreamSynchronize((hipStream_t)sift_get_stream(m->ctx[u]));
+    }
+  for (int i = 0; i < (int)m->gstream.size(); ++i)
+    if (m->gstream[i]) {
+      (void)hipSetDevice(m->dev[i]);
+      (void)hipStreamSynchronize(m->gstream[i]);
+    }
   for (int i = 0; i < (int)m->comm.size(); ++i)
     if (m->comm[i]) (void)ncclCommDestroy(m->comm[i]);
-  for (int i = 0; i < m->n; ++i) {
-    (void)hipSetDevice(m->dev[i]);
+  for (int u = 0; u < U; ++u) {
+    (void)hipSetDevice(m->dev[u / m->S]);
     for (int s = 0; s < 2; ++s) {
-      if (i < (int)m->cdone[s].size() && m->cdone[s][i]) (void)hipEventDestroy(m->cdone[s][i]);
-      if (i < (int)m->gdone[s].size() && m->gdone[s][i]) (void)hipEventDestroy(m->gdone[s][i]);
-      if (i < (int)m->kbuf[s].size() && m->kbuf[s][i]) (void)hipFree(m->kbuf[s][i]);
-      if (i < (int)m->dbuf[s].size() && m->dbuf[s][i]) (void)hipFree(m->dbuf[s][i]);
-      if (i < (int)m->doff[s].size() && m->doff[s][i]) (void)hipFree(m->doff[s][i]);
-      if (i < (int)m->hoff[s].size() && m->hoff[s][i]) (void)hipHostFree(m->hoff[s][i]);
+      if (m->cdone[s][u]) (void)hipEventDestroy(m->cdone[s][u]);
+      if (m->kbuf[s][u]) (void)hipFree(m->kbuf[s][u]);
+      if (m->dbuf[s][u]) (void)hipFree(m->dbuf[s][u]);
+      if (m->doff[s][u]) (void)hipFree(m->doff[s][u]);
+      if (m->hoff[s][u]) (void)hipHostFree(m->hoff[s][u]);
     }
-    if (i < (int)m->gstream.size() && m->gstream[i]) (void)hipStreamDestroy(m->gstream[i]);
-    if (i < (int)m->ctx.size() && m->ctx[i]) (void)sift_ctx_destroy(m->ctx[i]);
+    if (m->ctx[u]) (void)sift_ctx_destroy(m->ctx[u]);
+  }
+  for (int i = 0; i < (int)m->gstream.size(); ++i) {
+    (void)hipSetDevice(m->dev[i]);
+    for (int s = 0; s < 2; ++s)
+      if (m->gdone[s][i]) (void)hipEventDestroy(m->gdone[s][i]);
+    if (m->gstream[i]) (void)hipStreamDestroy(m->gstream[i]);
   }
   if (m->n > 0) {
     (void)hipSetDevice(m->dev[0]);
@@ -199,34 +218,40 @@ int sift_multi_destroy(sift_multi* m) {
 }
 
 int sift_multi_create(const int* devices, int n_devices, int max_rows, int max_cols, int max_batch_per_device,
-                      unsigned flags, int kp_cap_per_device, int gather_desc, sift_multi** out) {
+                      unsigned flags, int streams_per_device, int kp_cap_per_device, int gather_desc,
+                      sift_multi** out) {
   if (!out) return SIFT_E_INVALID;
   *out = nullptr;
-  if (!devices || n_devices < 1 || max_batch_per_device < 1 || kp_cap_per_device < 1) return SIFT_E_INVALID;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess) return SIFT_E_HIP;
-  for (int i = 0; i < n_devices; ++i) {
-    if (devices[i] < 0 || devices[i] >= ndev) return SIFT_E_INVALID;
+  if (!devices || n_devices < 1 || max_batch_per_device < 1 || kp_cap_per_device < 1 || streams_per_device < 0 ||
+      streams_per_device > 8)
+    return SIFT_E_INVALID;
+  for (int i = 0; i < n_devices; ++i)
     for (int j = 0; j < i; ++j)
       if (devices[j] == devices[i]) return SIFT_E_INVALID;  // RCCL: one rank per device
-  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) return SIFT_E_HIP;
+  for (int i = 0; i < n_devices; ++i)
+    if (devices[i] < 0 || devices[i] >= ndev) return SIFT_E_INVALID;
   if ((long long)kp_cap_per_device * n_devices > (1ll << 31) - 1) return SIFT_E_INVALID;
   sift_multi* m = new sift_multi;
   m->n = n_devices;
+  // default 2 sub-batches per device (bench.py's split); never more than images
+  m->S = std::max(1, std::min(streams_per_device ? streams_per_device : 2, max_batch_per_device));
+  const int U = n_devices * m->S;
   m->dev.assign(devices, devices + n_devices);
   m->max_batch = max_batch_per_device;
-  m->kp_cap = kp_cap_per_device;
+  m->cap = (kp_cap_per_device + m->S - 1) / m->S;
   m->gather_desc = gather_desc ? 1 : 0;
-  m->ctx.assign(n_devices, nullptr);
+  m->ctx.assign(U, nullptr);
   m->gstream.assign(n_devices, nullptr);
   for (int s = 0; s < 2; ++s) {
-    m->cdone[s].assign(n_devices, nullptr);
     m->gdone[s].assign(n_devices, nullptr);
-    m->kbuf[s].assign(n_devices, nullptr);
-    m->dbuf[s].assign(n_devices, nullptr);
-    m->doff[s].assign(n_devices, nullptr);
-    m->hoff[s].assign(n_devices, nullptr);
-    m->cnt[s].assign(n_devices, 0);
+    m->cdone[s].assign(U, nullptr);
+    m->kbuf[s].assign(U, nullptr);
+    m->dbuf[s].assign(U, nullptr);
+    m->doff[s].assign(U, nullptr);
+    m->hoff[s].assign(U, nullptr);
+    m->cnt[s].assign(U, 0);
   }
   auto bail = [&](int rc, const std::string& msg) {
     // the message outlives m: there is no context to hold it, so it is printed
@@ -234,29 +259,34 @@ int sift_multi_create(const int* devices, int n_devices, int max_rows, int max_c
     sift_multi_destroy(m);
     return rc;
   };
+  const int sub_batch = (max_batch_per_device + m->S - 1) / m->S;
   for (int i = 0; i < n_devices; ++i) {
-    int rc = sift_ctx_create(devices[i], max_rows, max_cols, max_batch_per_device, flags, &m->ctx[i]);
-    if (rc) return bail(rc, "sift_ctx_create on device " + std::to_string(devices[i]) + " failed");
     if (hipSetDevice(devices[i]) != hipSuccess ||
         hipStreamCreateWithFlags(&m->gstream[i], hipStreamNonBlocking) != hipSuccess)
       return bail(SIFT_E_HIP, "gather stream");
-    for (int s = 0; s < 2; ++s) {
-      if (hipEventCreateWithFlags(&m->cdone[s][i], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&m->gdone[s][i], hipEventDisableTiming) != hipSuccess ||
-          hipMalloc(&m->kbuf[s][i], sizeof(sift_keypoint) * (size_t)kp_cap_per_device) != hipSuccess ||
-          hipMalloc(&m->dbuf[s][i], sizeof(float) * SIFT_DESC_LEN * (size_t)kp_cap_per_device) != hipSuccess ||
-          hipMalloc(&m->doff[s][i], sizeof(int) * (size_t)(max_batch_per_device + 1)) != hipSuccess ||
-          hipHostMalloc(reinterpret_cast<void**>(&m->hoff[s][i]), sizeof(int) * (size_t)(max_batch_per_device + 1),
-                        hipHostMallocDefault) != hipSuccess)
-        return bail(SIFT_E_NOMEM, "per-device result slots");
+    for (int s = 0; s < 2; ++s)
       // slot s starts free: gdone[s] complete
-      if (hipEventRecord(m->gdone[s][i], m->gstream[i]) != hipSuccess) return bail(SIFT_E_HIP, "event");
+      if (hipEventCreateWithFlags(&m->gdone[s][i], hipEventDisableTiming) != hipSuccess ||
+          hipEventRecord(m->gdone[s][i], m->gstream[i]) != hipSuccess)
+        return bail(SIFT_E_HIP, "event");
+    for (int j = 0; j < m->S; ++j) {
+      const int u = i * m->S + j;
+      int rc = sift_ctx_create(devices[i], max_rows, max_cols, sub_batch, flags, &m->ctx[u]);
+      if (rc) return bail(rc, "sift_ctx_create on device " + std::to_string(devices[i]) + " failed");
+      if (hipSetDevice(devices[i]) != hipSuccess) return bail(SIFT_E_HIP, "hipSetDevice");
+      for (int s = 0; s < 2; ++s)
+        if (hipEventCreateWithFlags(&m->cdone[s][u], hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&m->kbuf[s][u], sizeof(sift_keypoint) * (size_t)m->cap) != hipSuccess ||
+            hipMalloc(&m->dbuf[s][u], sizeof(float) * SIFT_DESC_LEN * (size_t)m->cap) != hipSuccess ||
+            hipMalloc(&m->doff[s][u], sizeof(int) * (size_t)(sub_batch + 1)) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&m->hoff[s][u]), sizeof(int) * (size_t)(sub_batch + 1),
+                          hipHostMallocDefault) != hipSuccess)
+          return bail(SIFT_E_NOMEM, "per-context result slots");
     }
   }
   if (hipSetDevice(devices[0]) != hipSuccess ||
-      hipMalloc(&m->rk, sizeof(sift_keypoint) * (size_t)kp_cap_per_device * n_devices) != hipSuccess ||
-      (m->gather_desc &&
-       hipMalloc(&m->rd, sizeof(float) * SIFT_DESC_LEN * (size_t)kp_cap_per_device * n_devices) != hipSuccess))
+      hipMalloc(&m->rk, sizeof(sift_keypoint) * (size_t)m->cap * U) != hipSuccess ||
+      (m->gather_desc && hipMalloc(&m->rd, sizeof(float) * SIFT_DESC_LEN * (size_t)m->cap * U) != hipSuccess))
     return bail(SIFT_E_NOMEM, "device-0 gather buffers");
   m->comm.assign(n_devices, nullptr);
   const ncclResult_t r = ncclCommInitAll(m->comm.data(), n_devices, devices);
@@ -270,7 +300,25 @@ int sift_multi_create(const int* devices, int n_devices, int max_rows, int max_c
 
 sift_ctx* sift_multi_context(sift_multi* m, int index) {
   if (!m || index < 0 || index >= m->n) return nullptr;
-  return m->ctx[index];
+  return m->ctx[index * m->S];
+}
+
+int sift_multi_set_octaves(sift_multi* m, int n_octaves) {
+  if (!m) return SIFT_E_INVALID;
+  for (sift_ctx* c : m->ctx) {
+    const int rc = sift_set_octaves(c, n_octaves);
+    if (rc) return mfail(m, rc, sift_last_error(c));
+  }
+  return SIFT_OK;
+}
+
+int sift_multi_set_flags(sift_multi* m, unsigned flags) {
+  if (!m) return SIFT_E_INVALID;
+  for (sift_ctx* c : m->ctx) {
+    const int rc = sift_set_flags(c, flags);
+    if (rc) return mfail(m, rc, sift_last_error(c));
+  }
+  return SIFT_OK;
 }
 
 int sift_multi_step(sift_multi* m, const float* const* d_imgs, const int* counts, int rows, int cols,
@@ -281,20 +329,25 @@ int sift_multi_step(sift_multi* m, const float* const* d_imgs, const int* counts
     if (counts[i] < 0 || counts[i] > m->max_batch || (counts[i] > 0 && !d_imgs[i]))
       return mfail(m, SIFT_E_INVALID, "shard " + std::to_string(i) + ": bad image count or null buffer");
   const int s = (int)(m->steps & 1), p = s ^ 1;
-  for (int i = 0; i < m->n; ++i) {
-    MHIP(m, hipSetDevice(m->dev[i]));
-    hipStream_t cs = (hipStream_t)sift_get_stream(m->ctx[i]);
-    MHIP(m, hipStreamWaitEvent(cs, m->gdone[s][i], 0));  // step k - 2's gather has read slot s
-    m->cnt[s][i] = counts[i];
-    if (counts[i] > 0) {
-      const int rc = sift_detect_compute_batch(m->ctx[i], d_imgs[i], counts[i], rows, cols, row_stride, img_stride,
-                                               m->kbuf[s][i], m->dbuf[s][i], m->kp_cap, m->doff[s][i]);
-      if (rc) return mfail(m, rc, "device " + std::to_string(m->dev[i]) + ": " + sift_last_error(m->ctx[i]));
-      MHIP(m, hipMemcpyAsync(m->hoff[s][i], m->doff[s][i], sizeof(int) * (size_t)(counts[i] + 1),
-                             hipMemcpyDeviceToHost, cs));
+  for (int i = 0; i < m->n; ++i)
+    for (int j = 0; j < m->S; ++j) {
+      const int u = i * m->S + j;
+      const int first = (int)((long long)j * counts[i] / m->S);
+      const int c = (int)((long long)(j + 1) * counts[i] / m->S) - first;
+      MHIP(m, hipSetDevice(m->dev[i]));
+      hipStream_t cs = (hipStream_t)sift_get_stream(m->ctx[u]);
+      MHIP(m, hipStreamWaitEvent(cs, m->gdone[s][i], 0));  // step k - 2's gather has read slot s
+      m->cnt[s][u] = c;
+      if (c > 0) {
+        const int rc = sift_detect_compute_batch(m->ctx[u], d_imgs[i] + (size_t)first * img_stride, c, rows, cols,
+                                                 row_stride, img_stride, m->kbuf[s][u], m->dbuf[s][u], m->cap,
+                                                 m->doff[s][u]);
+        if (rc) return mfail(m, rc, "device " + std::to_string(m->dev[i]) + ": " + sift_last_error(m->ctx[u]));
+        MHIP(m, hipMemcpyAsync(m->hoff[s][u], m->doff[s][u], sizeof(int) * (size_t)(c + 1), hipMemcpyDeviceToHost,
+                               cs));
+      }
+      MHIP(m, hipEventRecord(m->cdone[s][u], cs));
     }
-    MHIP(m, hipEventRecord(m->cdone[s][i], cs));
-  }
   ++m->steps;
   if (m->pending) {
     const int rc = gather_slot(m, p);
@@ -316,8 +369,10 @@ int sift_multi_flush(sift_multi* m) {
   for (int i = 0; i < m->n; ++i) {
     MHIP(m, hipSetDevice(m->dev[i]));
     MHIP(m, hipStreamSynchronize(m->gstream[i]));
-    const int rc = sift_sync(m->ctx[i]);  // the sticky device status of every step
-    if (rc) return mfail(m, rc, "device " + std::to_string(m->dev[i]) + ": " + sift_last_error(m->ctx[i]));
+  }
+  for (int u = 0; u < (int)m->ctx.size(); ++u) {
+    const int rc = sift_sync(m->ctx[u]);  // the sticky device status of every step
+    if (rc) return mfail(m, rc, "device " + std::to_string(m->dev[u / m->S]) + ": " + sift_last_error(m->ctx[u]));
   }
   return SIFT_OK;
 }

@@ -109,7 +109,9 @@ def lib():
             "sift_knn_match_l1_device": (ip, [vp, vp, ip, vp, ip, ip, vp, vp]),
             "sift_multi_shard": (ip, [ip, ip, ip, pint, pint]),
             "sift_multi_merge_offsets": (ip, [ctypes.POINTER(pint), pint, ip, pint]),
-            "sift_multi_create": (ip, [pint, ip, ip, ip, ip, ctypes.c_uint, ip, ip, ctypes.POINTER(vp)]),
+            "sift_multi_create": (ip, [pint, ip, ip, ip, ip, ctypes.c_uint, ip, ip, ip, ctypes.POINTER(vp)]),
+            "sift_multi_set_octaves": (ip, [vp, ip]),
+            "sift_multi_set_flags": (ip, [vp, ctypes.c_uint]),
             "sift_multi_destroy": (ip, [vp]),
             "sift_multi_last_error": (ctypes.c_char_p, [vp]),
             "sift_multi_context": (vp, [vp, ip]),
@@ -397,13 +399,13 @@ class MultiContext:
     descriptors) gathered to devices[0] over RCCL one step behind."""
 
     def __init__(self, devices, max_rows: int, max_cols: int, max_batch_per_device: int, kp_cap_per_device: int,
-                 flags: int = 0, gather_desc: bool = False):
+                 flags: int = 0, gather_desc: bool = False, streams_per_device: int = 0):
         self._L = lib()
         self.devices = list(devices)
         dv = (ctypes.c_int * len(self.devices))(*self.devices)
         h = ctypes.c_void_p()
         rc = self._L.sift_multi_create(dv, len(self.devices), max_rows, max_cols, max_batch_per_device, flags,
-                                       kp_cap_per_device, int(gather_desc), ctypes.byref(h))
+                                       streams_per_device, kp_cap_per_device, int(gather_desc), ctypes.byref(h))
         if rc != SIFT_OK:
             raise SiftError("sift_multi_create", rc, "could not create the multi-GPU context (see stderr)")
         self.h = h
@@ -434,9 +436,10 @@ class MultiContext:
         return self._L.sift_multi_context(self.h, index)
 
     def set_octaves(self, n: int):
-        for i in range(len(self.devices)):
-            rc = self._L.sift_set_octaves(ctypes.c_void_p(self.context_handle(i)), n)
-            self._check("sift_set_octaves", rc)
+        self._check("sift_multi_set_octaves", self._L.sift_multi_set_octaves(self.h, n))
+
+    def set_flags(self, flags: int):
+        self._check("sift_multi_set_flags", self._L.sift_multi_set_flags(self.h, flags))
 
     def synth_images(self, index: int, out_ptr: int, batch: int, rows: int, cols: int, row_stride: int,
                      img_stride: int, seed_base: int = 0):

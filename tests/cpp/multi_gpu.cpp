@@ -5,6 +5,7 @@
 // first device over RCCL one step behind.  Prints one JSON line.
 //
 //   multi_gpu [--devices N] [--per-device B] [--steps K] [--warmup W] [--rows R --cols C]
+//             [--streams S]   (contexts / HIP streams per device, default 2)
 //
 // Built by tests/test_abi.py (g++, HIP runtime API only) and run at N = 1 by
 // tests/test_multi.py on the GPU box; INTEGRATION.md section 4 walks through it.
@@ -28,7 +29,7 @@
   } while (0)
 
 int main(int argc, char** argv) {
-  int ndev = 0, per = 64, steps = 5, warmup = 2, rows = 1080, cols = 1920;
+  int ndev = 0, per = 64, steps = 5, warmup = 2, rows = 1080, cols = 1920, streams = 2;
   for (int i = 1; i + 1 < argc; i += 2) {
     const int v = atoi(argv[i + 1]);
     if (!strcmp(argv[i], "--devices")) ndev = v;
@@ -37,6 +38,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--warmup")) warmup = v;
     else if (!strcmp(argv[i], "--rows")) rows = v;
     else if (!strcmp(argv[i], "--cols")) cols = v;
+    else if (!strcmp(argv[i], "--streams")) streams = v;
   }
   int visible = 0;
   if (hipGetDeviceCount(&visible) != hipSuccess || visible < 1) {
@@ -48,7 +50,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < ndev; ++i) devs[i] = i;
   sift_multi* m = nullptr;
   const int kp_cap = per * 40000;  // ~3x a textured 1080p image's keypoints
-  CHECK(sift_multi_create(devs.data(), ndev, rows, cols, per, 0, kp_cap, 0, &m));
+  CHECK(sift_multi_create(devs.data(), ndev, rows, cols, per, 0, streams, kp_cap, 0, &m));
   // every device synthesises its own shard of the global batch (image b of
   // the step has seed b): the images are resident in that device's HBM
   std::vector<float*> imgs(ndev, nullptr);
@@ -62,6 +64,10 @@ int main(int argc, char** argv) {
       return 1;
     }
     CHECK(sift_synth_images(sift_multi_context(m, i), imgs[i], counts[i], rows, cols, cols, plane, first));
+  }
+  for (int i = 0; i < ndev; ++i) {  // the images are ready before any context reads them
+    (void)hipSetDevice(devs[i]);
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
   }
   const float* const* ip = imgs.data();
   for (int s = 0; s < warmup; ++s) CHECK(sift_multi_step(m, ip, counts.data(), rows, cols, cols, plane));
@@ -79,9 +85,9 @@ int main(int argc, char** argv) {
   const double mpix = (double)steps * per * ndev * plane / 1e6;
   printf("{\"devices\": %d, \"images_per_step\": %d, \"steps\": %d, \"ms_per_step\": %.3f, \"Mpix_per_s\": %.1f, "
          "\"keypoints_per_s\": %.1f, \"gathered_keypoints_last_step\": %d, \"image0_keypoints\": %d, "
-         "\"rccl_version\": %d, \"p2p_transfers\": %lld}\n",
+         "\"rccl_version\": %d, \"p2p_transfers\": %lld, \"streams_per_device\": %d}\n",
          ndev, per * ndev, steps, sec / steps * 1e3, mpix / sec, (double)offs[batch_total] * steps / sec,
-         offs[batch_total], offs[1] - offs[0], sift_multi_rccl_version(), tr);
+         offs[batch_total], offs[1] - offs[0], sift_multi_rccl_version(), tr, streams);
   for (int i = 0; i < ndev; ++i) {
     (void)hipSetDevice(devs[i]);
     (void)hipFree(imgs[i]);

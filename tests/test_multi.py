@@ -55,7 +55,7 @@ def test_create_rejects_bad_device_lists(siftgpu):
     h = ctypes.c_void_p()
     for devs in ([], [0, 0]):
         dv = (ctypes.c_int * max(1, len(devs)))(*devs)
-        rc = L.sift_multi_create(dv, len(devs), 64, 64, 1, 0, 100, 0, ctypes.byref(h))
+        rc = L.sift_multi_create(dv, len(devs), 64, 64, 1, 0, 0, 100, 0, ctypes.byref(h))
         assert rc != siftgpu.SIFT_OK and not h.value
 
 
@@ -72,16 +72,18 @@ def _reference(siftgpu, torch, imgs, B, R, C, cap):
 
 
 @pytest.mark.gpu
-def test_multi_n1_equals_batch_call(siftgpu):
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_multi_n1_equals_batch_call(siftgpu, streams):
     """Three steps over two alternating image sets through the multi context
-    on device 0: after every step the previous step is gathered (RCCL self
-    p2p), after flush the last one; each equals one sift_detect_compute_batch
-    call on the same images, records, descriptors and offsets byte for byte."""
+    on device 0, the shard split over 1-3 contexts/streams: after every step
+    the previous step is gathered (RCCL self p2p, one transfer per context),
+    after flush the last one; each equals one sift_detect_compute_batch call
+    on the same images, records, descriptors and offsets byte for byte."""
     import torch
     R, C, B, cap = 240, 320, 4, 20000
     sets = [torch.empty((B, R, C), dtype=torch.float32, device="cuda") for _ in range(2)]
     assert siftgpu.rccl_version() >= 20000
-    with siftgpu.MultiContext([0], R, C, B, cap, gather_desc=True) as m:
+    with siftgpu.MultiContext([0], R, C, B, cap, gather_desc=True, streams_per_device=streams) as m:
         for j, t in enumerate(sets):
             m.synth_images(0, t.data_ptr(), B, R, C, C, R * C, seed_base=10 * j)
         torch.cuda.synchronize()
@@ -104,7 +106,7 @@ def test_multi_n1_equals_batch_call(siftgpu):
         assert st == len(order) - 1 and offs.tolist() == ro.tolist()
         assert kp_bytes(kps).tobytes() == rk.tobytes() and desc.tobytes() == rd.tobytes()
         s = m.stats()
-        assert s["steps"] == 3 and s["transfers"] == 6 and s["records"] == sum(
+        assert s["steps"] == 3 and s["transfers"] == 6 * streams and s["records"] == sum(
             int(refs[j][2][B]) for j in order)
 
 
@@ -119,6 +121,7 @@ def test_multi_configs3_shard_shape_1080p(siftgpu):
     imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
     with siftgpu.MultiContext([0], R, C, B, B * 40000, gather_desc=True) as m:
         m.synth_images(0, imgs.data_ptr(), B, R, C, C, R * C, seed_base=0)
+        torch.cuda.synchronize()   # the images are ready before the step's contexts read them
         for _ in range(2):
             m.step([imgs.data_ptr()], [B], R, C, C, R * C)
         m.flush()
@@ -138,6 +141,6 @@ def test_cpp_multi_gpu_host_runs(siftgpu, tmp_path):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d["devices"] == 1 and d["images_per_step"] == 4 and d["p2p_transfers"] == 3
+    assert d["devices"] == 1 and d["images_per_step"] == 4 and d["p2p_transfers"] == 3 * 2   # 2 streams
     assert d["image0_keypoints"] == int(load_golden("synth0_1080x1920")["n"])
     assert d["gathered_keypoints_last_step"] > 4 * 10000 and d["rccl_version"] >= 20000
