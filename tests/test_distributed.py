@@ -230,14 +230,17 @@ def test_gather_keypoints_world2():
     assert uneven_default == uneven
 
 
-def test_pipelined_parts_world2():
+@pytest.mark.parametrize("world", [2, 8])
+def test_pipelined_parts(world):
     """Two sub-batches per rank, each gathered one step behind by its own
-    pipeline (bench.py --streams at N > 1): every part's every step arrives."""
-    procs, q = _spawn(_parts_worker)
+    pipeline (bench.py --streams at N > 1): every part's every step arrives
+    -- at world 2 and at the 8 ranks of configs[3] (a gloo rehearsal of the
+    node the driver's scaling bench runs on)."""
+    procs, q = _spawn(_parts_worker, world)
     try:
-        ok = q.get(timeout=120)
+        ok = q.get(timeout=240)
     finally:
         for p in procs:
-            p.join(timeout=60)
-    assert [p.exitcode for p in procs] == [0, 0]
+            p.join(timeout=120)
+    assert [p.exitcode for p in procs] == [0] * world
     assert ok

@@ -15,7 +15,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 ARGS="$@"
-RE="descriptor_kernel|blur_octave_kernel|blur_sym_kernel|orient_kernel|orient_slots_kernel|orient_bin_kernel|dog_extrema_kernel|extrema_walk_kernel|refine_kernel"
+RE="descriptor_kernel|blur_octave_kernel|blur_sym_kernel|orient_slots_kernel|orient_bin_kernel|extrema_walk_kernel|refine_kernel"
 GA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
 GB="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM"
 GC="GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_SMEM SQ_WAIT_INST_LDS TCC_HIT_sum TCC_MISS_sum"
