@@ -182,7 +182,10 @@ int sift_multi_set_flags(sift_multi* m, unsigned flags);
 int sift_multi_step(sift_multi* m, const float* const* d_imgs, const int* counts, int rows, int cols,
                     size_t row_stride, size_t img_stride);
 /* Gathers the last step, drains every stream and reports the contexts' sticky
- * status (as sift_sync). */
+ * status (as sift_sync).  A step or flush that fails after enqueueing work
+ * (a device error, a keypoint count above a context's share of
+ * kp_cap_per_device) leaves the result slots undefined: later steps and
+ * flushes return SIFT_E_INVALID and the multi context must be destroyed. */
 int sift_multi_flush(sift_multi* m);
 /* The last gathered step on devices[0]: device pointers to its records (and
  * descriptors, or NULL without gather_desc) in global image order, and the

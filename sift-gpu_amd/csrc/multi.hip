@@ -61,6 +61,8 @@ struct sift_multi {
   bool pending = false;      // the last enqueued step is not gathered yet
   long long records = 0, transfers = 0;  // totals gathered (records, p2p ops)
   std::string err;
+  std::string broken;        // set when a step or gather failed after enqueueing work: the slots'
+                             // state is then undefined and every later step / flush refuses
 };
 
 extern "C" int sift_multi_merge_offsets(const int* const* shard_offsets, const int* counts, int n_devices,
@@ -321,13 +323,34 @@ int sift_multi_set_flags(sift_multi* m, unsigned flags) {
   return SIFT_OK;
 }
 
+static int step_impl(sift_multi* m, const float* const* d_imgs, const int* counts, int rows, int cols, size_t row_stride,
+              size_t img_stride);
+static int flush_impl(sift_multi* m);
+
 int sift_multi_step(sift_multi* m, const float* const* d_imgs, const int* counts, int rows, int cols,
                     size_t row_stride, size_t img_stride) {
   if (!m) return SIFT_E_INVALID;
+  if (!m->broken.empty()) return mfail(m, SIFT_E_INVALID, "a previous step failed (" + m->broken + "): destroy the multi context");
   if (!d_imgs || !counts) return mfail(m, SIFT_E_INVALID, "null argument");
   for (int i = 0; i < m->n; ++i)
     if (counts[i] < 0 || counts[i] > m->max_batch || (counts[i] > 0 && !d_imgs[i]))
       return mfail(m, SIFT_E_INVALID, "shard " + std::to_string(i) + ": bad image count or null buffer");
+  const int rc = step_impl(m, d_imgs, counts, rows, cols, row_stride, img_stride);
+  if (rc) m->broken = m->err;
+  return rc;
+}
+
+int sift_multi_flush(sift_multi* m) {
+  if (!m) return SIFT_E_INVALID;
+  if (!m->broken.empty()) return mfail(m, SIFT_E_INVALID, "a previous step failed (" + m->broken + "): destroy the multi context");
+  const int rc = flush_impl(m);
+  // the contexts' sticky device errors (sift_sync) leave every stream drained and the slots consistent
+  if (rc && m->pending) m->broken = m->err;
+  return rc;
+}
+
+static int step_impl(sift_multi* m, const float* const* d_imgs, const int* counts, int rows, int cols, size_t row_stride,
+              size_t img_stride) {
   const int s = (int)(m->steps & 1), p = s ^ 1;
   for (int i = 0; i < m->n; ++i)
     for (int j = 0; j < m->S; ++j) {
@@ -358,8 +381,7 @@ int sift_multi_step(sift_multi* m, const float* const* d_imgs, const int* counts
   return SIFT_OK;
 }
 
-int sift_multi_flush(sift_multi* m) {
-  if (!m) return SIFT_E_INVALID;
+static int flush_impl(sift_multi* m) {
   if (m->pending) {
     const int rc = gather_slot(m, (int)((m->steps - 1) & 1));
     if (rc) return rc;

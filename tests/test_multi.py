@@ -144,3 +144,29 @@ def test_cpp_multi_gpu_host_runs(siftgpu, tmp_path):
     assert d["devices"] == 1 and d["images_per_step"] == 4 and d["p2p_transfers"] == 3 * 2   # 2 streams
     assert d["image0_keypoints"] == int(load_golden("synth0_1080x1920")["n"])
     assert d["gathered_keypoints_last_step"] > 4 * 10000 and d["rccl_version"] >= 20000
+
+
+@pytest.mark.gpu
+def test_multi_capacity_overflow_is_reported_and_final(siftgpu):
+    """A context's share of kp_cap_per_device too small for its sub-batch:
+    the gather reports SIFT_E_CAPACITY naming the device, and the multi
+    context refuses every later step (its slots are undefined) until it is
+    destroyed; a new one works."""
+    import torch
+    R, C, B = 240, 320, 2
+    imgs = torch.empty((B, R, C), dtype=torch.float32, device="cuda")
+    with siftgpu.MultiContext([0], R, C, B, 20, streams_per_device=2) as m:
+        m.synth_images(0, imgs.data_ptr(), B, R, C, C, R * C, seed_base=3)
+        torch.cuda.synchronize()
+        m.step([imgs.data_ptr()], [B], R, C, C, R * C)
+        with pytest.raises(siftgpu.SiftError) as ex:
+            m.flush()
+        assert ex.value.code == siftgpu.SIFT_E_CAPACITY and "kp_cap_per_device" in str(ex.value)
+        with pytest.raises(siftgpu.SiftError) as ex:
+            m.step([imgs.data_ptr()], [B], R, C, C, R * C)
+        assert ex.value.code == siftgpu.SIFT_E_INVALID and "destroy" in str(ex.value)
+    with siftgpu.MultiContext([0], R, C, B, 20000) as m:
+        m.step([imgs.data_ptr()], [B], R, C, C, R * C)
+        m.flush()
+        _, _, offs, _ = m.gathered(B + 1)
+    assert offs[-1] > 20
