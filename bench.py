@@ -416,8 +416,8 @@ def c_abi_multi_leg(env, steps, warmup):
     """configs[3]'s C++-host path on this GPU alone: the headline batch
     (--batch images, this rank's synthetic images) through sift_multi_step on
     one device -- --streams contexts and HIP streams as in the headline, graph
-    replay, the records gathered one step behind by RCCL's self send/recv --
-    timed like a leg (flush inside the timed region).  The rate beside `value` shows what the C ABI's multi path
+    replay, the records gathered one step behind (device 0's own pieces by
+    DMA copy) -- timed like a leg (flush inside the timed region).  The rate beside `value` shows what the C ABI's multi path
     costs against bench.py's two-stream Python driver."""
     a = env.a
     B, R, C = env.B, env.R, env.C
@@ -437,12 +437,12 @@ def c_abi_multi_leg(env, steps, warmup):
         st = m.stats()
     return {"n_devices": 1, "streams_per_device": env.S, "Mpix_per_s": round(B * R * C * steps / 1e6 / dt, 2),
             "ms_per_step": round(dt / steps * 1e3, 3), "keypoints_per_step": int(offs[-1]),
-            "rccl_version": siftgpu.rccl_version(), "p2p_transfers": st["transfers"],
+            "rccl_version": siftgpu.rccl_version(), "rccl_p2p_transfers": st["transfers"],
             "records_gathered": st["records"],
             "note": "sift_multi_create/_step/_flush (include/sift_hip.h) on this one GPU: the shard as "
                     "streams_per_device sub-batches on their own contexts and HIP streams, the 28-B records "
-                    "gathered to device 0 one step behind over RCCL (self send/recv at n = 1); "
-                    "tests/cpp/multi_gpu.cpp is the same path from C++"}
+                    "gathered to device 0 one step behind (other devices over RCCL p2p; device 0's own by DMA "
+                    "copy, so no RCCL transfer at n = 1); tests/cpp/multi_gpu.cpp is the same path from C++"}
 
 
 # ---- knnMatch leg ---------------------------------------------

@@ -146,6 +146,8 @@ int sift_synth_images(sift_ctx* ctx, float* d_out, int batch, int rows, int cols
  * RCCL (ncclSend / ncclRecv, xGMI) one step behind the compute.  One process
  * drives every device (ncclCommInitAll); a multi context is not thread-safe. */
 typedef struct sift_multi sift_multi;
+#define SIFT_MULTI_SELF_P2P 0x100u /* sift_multi_create flag: device 0's own records also go through RCCL
+                                      (self send/recv) instead of a DMA copy -- tests the p2p path on one GPU */
 /* Shard arithmetic: device `index` of n takes the contiguous images
  * [*first, *first + *count) = [floor(index * batch / n), floor((index + 1) * batch / n)).
  * No GPU needed. */
@@ -197,7 +199,8 @@ int sift_multi_gathered(sift_multi* m, const sift_keypoint** d_kpts, const float
  * NULL): *n_out gets the record count; SIFT_E_CAPACITY if cap < count.
  * Synchronous. */
 int sift_multi_copy_gathered(sift_multi* m, sift_keypoint* kpts, float* desc, int cap, int* n_out);
-/* Steps enqueued, records gathered and p2p transfers posted so far. */
+/* Steps enqueued, records gathered and RCCL p2p transfers posted so far
+ * (device 0's own pieces are DMA copies unless SIFT_MULTI_SELF_P2P). */
 int sift_multi_stats(const sift_multi* m, long long* steps, long long* records, long long* transfers);
 /* RCCL's NCCL_VERSION_CODE at run time (ncclGetVersion), -1 on error. */
 int sift_multi_rccl_version(void);

@@ -22,7 +22,8 @@
 //       device), ncclSend of device i's records (28 B each, optionally the
 //       512 B descriptors) and the matching ncclRecv on device 0 at exact
 //       sizes -- point-to-point, so the xGMI links of all peers run at once
-//       rather than as a ring; gdone[i][p] marks slot p free again.
+//       rather than as a ring (device 0's own pieces: a DMA copy); gdone[i][p]
+//       marks slot p free again.
 //   flush: the gather of the last step, then every stream is drained and the
 //     contexts' sticky status reported.
 //
@@ -59,7 +60,9 @@ struct sift_multi {
   long long steps = 0;       // steps enqueued
   long long gathered = -1;   // step index held by rk / goff (-1: none)
   bool pending = false;      // the last enqueued step is not gathered yet
-  long long records = 0, transfers = 0;  // totals gathered (records, p2p ops)
+  long long records = 0, transfers = 0;  // totals gathered (records, RCCL p2p ops)
+  long long local_copies = 0;            // device 0's own pieces copied by DMA
+  bool self_p2p = false;                 // SIFT_MULTI_SELF_P2P: device 0's pieces over RCCL too
   std::string err;
   std::string broken;        // set when a step or gather failed after enqueueing work: the slots'
                              // state is then undefined and every later step / flush refuses
@@ -113,14 +116,32 @@ int gather_slot(sift_multi* m, int p) {
     MHIP(m, hipSetDevice(m->dev[u / m->S]));
     MHIP(m, hipStreamWaitEvent(m->gstream[u / m->S], m->cdone[p][u], 0));
   }
-  MNCCL(m, ncclGroupStart());
+  // device 0's own sub-batches: a DMA copy on its gather stream (RCCL's self
+  // p2p runs a copy kernel on the CUs at a few GB/s: 2.7 ms for 12 MB of
+  // records, profiles/r6fin_summary.md); SIFT_MULTI_SELF_P2P keeps them on
+  // RCCL too (tests: the p2p path on a one-GPU box)
   long long at = 0;
-  for (int u = 0; u < U; ++u) {
+  if (!m->self_p2p) {
+    MHIP(m, hipSetDevice(m->dev[0]));
+    for (int u = 0; u < m->S; ++u) {
+      if (nrec[u] > 0) {
+        MHIP(m, hipMemcpyAsync(m->rk + at, m->kbuf[p][u], (size_t)nrec[u] * sizeof(sift_keypoint),
+                               hipMemcpyDeviceToDevice, m->gstream[0]));
+        if (m->gather_desc)
+          MHIP(m, hipMemcpyAsync(m->rd + at * SIFT_DESC_LEN, m->dbuf[p][u],
+                                 (size_t)nrec[u] * SIFT_DESC_LEN * sizeof(float), hipMemcpyDeviceToDevice,
+                                 m->gstream[0]));
+        m->local_copies += m->gather_desc ? 2 : 1;
+      }
+      at += nrec[u];
+    }
+  }
+  MNCCL(m, ncclGroupStart());
+  for (int u = m->self_p2p ? 0 : m->S; u < U; ++u) {
     const int i = u / m->S;
     if (nrec[u] > 0) {
-      // device i sends, device 0 receives at the record offset of unit u
-      // (device 0 to itself as well: one code path, RCCL's self p2p); the
-      // pairs between two devices match in posting order
+      // device i sends, device 0 receives at the record offset of unit u;
+      // the pairs between two devices match in posting order
       ncclResult_t r = ncclSend(m->kbuf[p][u], (size_t)nrec[u] * sizeof(sift_keypoint), ncclUint8, 0, m->comm[i],
                                 m->gstream[i]);
       if (r == ncclSuccess)
@@ -244,6 +265,8 @@ int sift_multi_create(const int* devices, int n_devices, int max_rows, int max_c
   m->max_batch = max_batch_per_device;
   m->cap = (kp_cap_per_device + m->S - 1) / m->S;
   m->gather_desc = gather_desc ? 1 : 0;
+  m->self_p2p = (flags & SIFT_MULTI_SELF_P2P) != 0;
+  flags &= ~SIFT_MULTI_SELF_P2P;  // not a context flag
   m->ctx.assign(U, nullptr);
   m->gstream.assign(n_devices, nullptr);
   for (int s = 0; s < 2; ++s) {

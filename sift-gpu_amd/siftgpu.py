@@ -32,6 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libsift_hip.so")
 
 SIFT_OK, SIFT_E_INVALID, SIFT_E_HIP, SIFT_E_CAPACITY, SIFT_E_SIZE, SIFT_E_NOMEM = 0, -1, -2, -3, -4, -5
+SIFT_MULTI_SELF_P2P = 0x100  # sift_multi_create: device 0's own records over RCCL too (tests)
 SIFT_E_WORKSPACE = -6  # internal candidate workspace overflow: an error, never the sizing case
 SIFT_FLAG_FAST, SIFT_FLAG_PROFILE, SIFT_FLAG_VERBOSE, SIFT_FLAG_NO_GRAPH = 0x1, 0x2, 0x4, 0x8
 N_SCALES, N_DOG, DESC_LEN = 5, 4, 128
