@@ -21,6 +21,12 @@
 //    bins the fold reads; a border-bin update carries +0.0 into an interior
 //    bin), so all 64 lanes of an update hit distinct banks and a wave needs
 //    5.1 KB, not 11.5 KB.
+//  * One image (round 6): a keypoint's window is split over 2 groups by the
+//    half of the interior rows its bins lie in (window parts, PARTS); each
+//    group walks only the samples that reach its bins, in raster order, so a
+//    keypoint's longest owner chain is ~0.6 of its window.  (Plain LDS
+//    read-modify-writes: ds_add_f32 is bit-exact here but took the batch
+//    descriptor from 5.6 to 50.9 ms; profiles/r6_desc_one_image_ab.txt.)
 //  * Fold, 0.2 clamp, uchar quantisation, RootSIFT (src/sift.cpp:676-721)
 //    keep the reference's sequential sums (lane 0 of the group).
 #include "common.hpp"
@@ -75,13 +81,16 @@ struct DescArgs {
 // inv_a = 1 / a (per keypoint): the bounds only have to enclose the samples
 // the exact predicate keeps, and the margin (>= 0.057 in j for |a| <= 1/5.7)
 // dwarfs the rounding of a multiply by the reciprocal.
-__device__ __forceinline__ void slab(float a, float inv_a, float b, int& lo, int& hi) {
-  const float lim = 2.5f + 1e-2f;  // margin >> float rounding of r_rot / c_rot
+// A window part (PARTS = 4, below) narrows |.| < 2.5 to (lim_lo, lim_hi).
+__device__ __forceinline__ void slab(float a, float inv_a, float b, int& lo, int& hi, float lim_lo = -2.5f,
+                                     float lim_hi = 2.5f) {
+  const float m = 1e-2f;  // margin >> float rounding of r_rot / c_rot
+  const float l0 = lim_lo - m, l1 = lim_hi + m;
   if (fabsf(a) < 1e-12f) {
-    if (!(fabsf(b) < lim)) hi = lo - 1;
+    if (!(b > l0 && b < l1)) hi = lo - 1;
     return;
   }
-  float x0 = (-lim - b) * inv_a, x1 = (lim - b) * inv_a;
+  float x0 = (l0 - b) * inv_a, x1 = (l1 - b) * inv_a;
   if (x0 > x1) {
     const float t = x0;
     x0 = x1;
@@ -120,10 +129,15 @@ struct RecT {  // one lane's 8 corner records
 // (profiles/r4_desc_pf2_ab.txt; three batches ahead, 38 spills: 5.56-5.58 vs
 // 5.50-5.51, round 5).  WPE: waves per SIMD the registers are budgeted for
 // (PF = 2 at 4: 128 VGPRs, the spills outside the sample loop).
-template <bool DET, int PF, int WPE>
+// PARTS = 4 (one image, round 6): a keypoint's window is split over four
+// groups of one wave by the half of the interior rows and columns its bins lie
+// in; see "Window parts" below.
+template <bool DET, int PF, int WPE, int PARTS = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 descriptor_kernel(DescArgs A) {
   static_assert(PF == 1 || PF == 2, "one or two sample batches in flight");
+  static_assert(PARTS == 1 || ((PARTS == 2 || PARTS == 4 || PARTS == 8) && DET), "window parts: detected keypoints (row table) only");
+  constexpr int kKpw = kGrp / PARTS;  // keypoints per wave
   // [qidx][group*8 + parity]
   constexpr int kHistRows = kQBins;
   __shared__ float hist[kHistRows * 64];
@@ -158,19 +172,53 @@ descriptor_kernel(DescArgs A) {
   // per-chunk XOR by c itself repeats every two passes at 16 chunks a pass:
   // 6.31 vs 5.85 ms, the waves alive 72 % of the launch instead of 79 %).
   // Keypoints are independent; only the processing order changes.
+  // (PARTS = 4: one image, keypoints in their own order, kKpw per wave)
   const int per = ((n + 7) / 8 + kRankChunk - 1) / kRankChunk * kRankChunk;
-  const int k0 = xcd * per;
-  const int kend = min(n, (xcd + 1) * per);
-  const int nsb = (max(kend - k0, 0) + kRankChunk - 1) / kRankChunk * kSubPerChunk;
-  for (int sb = slot; sb < nsb; sb += nslot) {
-    {
+  const int k0 = PARTS > 1 ? 0 : xcd * per;
+  const int kend = PARTS > 1 ? n : min(n, (xcd + 1) * per);
+  const int nch = (n + kRankChunk - 1) / kRankChunk;
+  const int nsb = PARTS > 1 ? (A.perm ? nch * (kRankChunk / kKpw) : (n + kKpw - 1) / kKpw)
+                            : (max(kend - k0, 0) + kRankChunk - 1) / kRankChunk * kSubPerChunk;
+  for (int sb = PARTS > 1 ? (int)blockIdx.x : slot; sb < nsb; sb += PARTS > 1 ? (int)gridDim.x : nslot) {
+    if constexpr (PARTS > 1) {
+      if (A.perm) {
+        // largest windows first over the whole launch: sub-batch sb takes ranks
+        // kKpw j .. from the top of chunk sb % nch (j = sb / nch)
+        const int c = sb % nch, j = sb / nch;
+        const int clen = min(kRankChunk, n - c * kRankChunk), r = clen - 1 - (j * kKpw + lane);
+        if (lane < kKpw) sord[lane] = r >= 0 ? A.perm[c * kRankChunk + r] : kend;
+      } else {
+        const int i = sb * kKpw + lane;
+        if (lane < kKpw) sord[lane] = i < kend ? i : kend;
+      }
+      wave_sync_d();
+    } else {
       const int ch = sb / kSubPerChunk;
       const int pos = (sb % kSubPerChunk) ^ (int)(((unsigned)ch * 0x9E3779B1u) >> (32 - kSubBits));
       const int i = k0 + ch * kRankChunk + pos * kGrp + lane;
       if (lane < kGrp) sord[lane] = i < kend ? (A.perm ? A.perm[i] : i) : kend;
       wave_sync_d();
     }
-    const int k = sord[g];
+    const int kslot = g / PARTS;            // this group's keypoint among the wave's kKpw
+    const bool lead = g % PARTS == 0;       // the group that normalises and stores it
+    // Window parts (PARTS = 4): part (hr, hc) of a keypoint owns the interior
+    // bins with R >> 1 == hr and C >> 1 == hc.  A sample reaches them only
+    // from base corners Rm in [2 hr - 1, 2 hr + 1] -- rbin in [2 hr - 1,
+    // 2 hr + 2), r_rot in [2 hr - 2.5, 2 hr + 0.5) -- likewise for columns, so
+    // the part walks the samples of that sub-square (slab limits below, ~36 %
+    // of the window), in raster order, and masks the corners outside its
+    // bins like those outside the interior: each of its bins sums the same
+    // samples in the same order as a whole-window walk, and a keypoint's
+    // longest chain is ~0.36 of the window's.
+    // (PARTS = 8: part (rq, hc) owns the row R == rq alone: Rm in {rq - 1, rq},
+    // r_rot in [rq - 2.5, rq - 0.5))
+    // (PARTS = 2: part hr owns the row half alone, all columns)
+    const int hr = PARTS == 4 ? (g >> 1) & 1 : PARTS == 2 ? g & 1 : 0, hc = PARTS >= 4 ? g & 1 : 0;
+    const int rq = PARTS == 8 ? g >> 1 : 0;
+    const float rlim_lo = PARTS == 8 ? rq - 2.5f : PARTS > 1 ? 2.f * hr - 2.5f : -2.5f;
+    const float rlim_hi = PARTS == 8 ? rq - 0.5f : PARTS > 1 ? 2.f * hr + 0.5f : 2.5f;
+    const float clim_lo = PARTS >= 4 ? 2.f * hc - 2.5f : -2.5f, clim_hi = PARTS >= 4 ? 2.f * hc + 0.5f : 2.5f;
+    const int k = sord[kslot];
     bool active = k < kend;
     int b = 0, oi = 0, layer = 0;
     sift_keypoint kp{};
@@ -234,8 +282,8 @@ descriptor_kernel(DescArgs A) {
         const int i = ri - radius;
         int lo = max(-radius, 1 - px), hi = min(radius, cols - 2 - px);  // 0 < px + j < cols-1
         if (!(py + i > 0 && py + i < rows - 1)) hi = lo - 1;
-        slab(sin_t, inv_sin, i * cos_t, lo, hi);     // r_rot = j*sin_t + i*cos_t
-        slab(cos_t, inv_cos, -(i * sin_t), lo, hi);  // c_rot = j*cos_t - i*sin_t
+        slab(sin_t, inv_sin, i * cos_t, lo, hi, rlim_lo, rlim_hi);     // r_rot = j*sin_t + i*cos_t
+        slab(cos_t, inv_cos, -(i * sin_t), lo, hi, clim_lo, clim_hi);  // c_rot = j*cos_t - i*sin_t
         const int len = hi >= lo ? hi - lo + 1 : 0;
         rows_tab[g][ri] = (int)(((unsigned)lo << 16) | (unsigned)len);  // |lo| <= 40
         cnt += len;
@@ -406,15 +454,21 @@ descriptor_kernel(DescArgs A) {
       // bin: an exact no-op, every bin is >= +0) instead of going to a trash
       // bin; each weight is masked after every product that uses its
       // unmasked value, so the interior corners' values are unchanged
-      v_r0 = X >= 1 ? v_r0 : 0.f;  // Rm >= 0
-      v_r1 = X <= 3 ? v_r1 : 0.f;  // Rm <= 2
+      // (PARTS = 4: outside the part's rows R in {2 hr, 2 hr + 1} -- the corner
+      // R = Rm = X - 1 for dr = 0, R = X for dr = 1 -- and columns likewise)
+      const bool r0_in = PARTS == 8 ? X == rq + 1 : PARTS > 1 ? (unsigned)(X - 2 * hr - 1) <= 1u : X >= 1;  // Rm >= 0
+      const bool r1_in = PARTS == 8 ? X == rq : PARTS > 1 ? (unsigned)(X - 2 * hr) <= 1u : X <= 3;          // Rm <= 2
+      const bool c0_in = PARTS >= 4 ? (unsigned)(Y - 2 * hc - 1) <= 1u : Y >= 1;
+      const bool c1_in = PARTS >= 4 ? (unsigned)(Y - 2 * hc) <= 1u : Y <= 3;
+      v_r0 = r0_in ? v_r0 : 0.f;
+      v_r1 = r1_in ? v_r1 : 0.f;
       float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
       float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
       // and outside the interior columns
-      v_rc00 = Y >= 1 ? v_rc00 : 0.f;
-      v_rc10 = Y >= 1 ? v_rc10 : 0.f;
-      v_rc01 = Y <= 3 ? v_rc01 : 0.f;
-      v_rc11 = Y <= 3 ? v_rc11 : 0.f;
+      v_rc00 = c0_in ? v_rc00 : 0.f;
+      v_rc10 = c0_in ? v_rc10 : 0.f;
+      v_rc01 = c1_in ? v_rc01 : 0.f;
+      v_rc11 = c1_in ? v_rc11 : 0.f;
       float v[8];
       v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
       v[6] = v_rc11 - v[7];
@@ -618,56 +672,85 @@ descriptor_kernel(DescArgs A) {
       for (int base = 0; base < nmax; base += 8) step(base, loc_nxt, loc_alt);
     }
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
-    float cell[2][8];
+    float* dv = hist + kslot * (kDescLen + 4);  // the 128-vector reuses histogram storage
+    if constexpr (PARTS > 1) {
+      // a part's 4 (PARTS = 8: 2) cells: lane q takes one cell and NO = 4 (2)
+      // of its orientations, the first of them adding the two wrap bins
+      // (PARTS = 2: 8 cells, lane q takes cell q whole)
+      constexpr int NO = PARTS == 8 ? 2 : PARTS == 4 ? 4 : 8;
+      const int R = PARTS == 8 ? rq : PARTS == 4 ? 2 * hr + ((q >> 2) & 1) : 2 * hr + (q >> 2);
+      const int C = PARTS == 8 ? 2 * hc + ((q >> 2) & 1) : PARTS == 4 ? 2 * hc + ((q >> 1) & 1) : q & 3;
+      const int oh = PARTS == 8 ? q & 3 : PARTS == 4 ? q & 1 : 0;
+      float cl[NO];
 #pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const int cidx = q + 8 * h2;
-      const int R = cidx / d, C = cidx % d;  // interior coordinates R' = R-1, C' = C-1
-#pragma unroll
-      for (int o = 0; o < nb + 2; ++o) {
+      for (int u = 0; u < NO; ++u) {
+        const int o = NO * oh + u;
         const int par = ((R & 1) << 2) | ((C & 1) << 1) | (o & 1);
-        const float hv = hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
-        if (o < nb)
-          cell[h2][o] = hv;
-        else
-          cell[h2][o - nb] = cell[h2][o - nb] + hv;
+        cl[u] = hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
       }
+      if (oh == 0) {
+#pragma unroll
+        for (int o = nb; o < nb + 2; ++o) {
+          const int par = ((R & 1) << 2) | ((C & 1) << 1) | (o & 1);
+          cl[o - nb] = cl[o - nb] + hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
+        }
+      }
+      wave_sync_d();
+#pragma unroll
+      for (int u = 0; u < NO; ++u) dv[(R * d + C) * nb + NO * oh + u] = cl[u];
+    } else {
+      float cell[2][8];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int cidx = q + 8 * h2;
+        const int R = cidx / d, C = cidx % d;  // interior coordinates R' = R-1, C' = C-1
+#pragma unroll
+        for (int o = 0; o < nb + 2; ++o) {
+          const int par = ((R & 1) << 2) | ((C & 1) << 1) | (o & 1);
+          const float hv = hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
+          if (o < nb)
+            cell[h2][o] = hv;
+          else
+            cell[h2][o - nb] = cell[h2][o - nb] + hv;
+        }
+      }
+      wave_sync_d();
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int t = 0; t < nb; ++t) dv[(q + 8 * h2) * nb + t] = cell[h2][t];
     }
-    wave_sync_d();
-    float* dv = hist + g * (kDescLen + 4);  // the 128-vector reuses histogram storage
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-      for (int t = 0; t < nb; ++t) dv[(q + 8 * h2) * nb + t] = cell[h2][t];
     wave_sync_d();
     // ---- hysteresis + quantisation + RootSIFT (src/sift.cpp:689-721) ----
-    if (q == 0) {
+    if (q == 0 && lead) {
       float nrm2 = 0;
       for (int t = 0; t < kDescLen; ++t) nrm2 = nrm2 + dv[t] * dv[t];
-      bc[g][0] = sqrtf(nrm2) * 0.2f;
+      bc[kslot][0] = sqrtf(nrm2) * 0.2f;
     }
     wave_sync_d();
-    const float thr = bc[g][0];
-    for (int t = q; t < kDescLen; t += 8) dv[t] = dv[t] < thr ? dv[t] : thr;
+    const float thr = bc[kslot][0];
+    if (lead)
+      for (int t = q; t < kDescLen; t += 8) dv[t] = dv[t] < thr ? dv[t] : thr;
     wave_sync_d();
-    if (q == 0) {
+    if (q == 0 && lead) {
       float nrm2 = 0;
       for (int t = 0; t < kDescLen; ++t) nrm2 = nrm2 + dv[t] * dv[t];
       const float sq = sqrtf(nrm2);
-      bc[g][1] = 512.f / (sq < FLT_EPSILON ? FLT_EPSILON : sq);
+      bc[kslot][1] = 512.f / (sq < FLT_EPSILON ? FLT_EPSILON : sq);
     }
     wave_sync_d();
-    const float nrm2s = bc[g][1];
-    for (int t = q; t < kDescLen; t += 8) dv[t] = sat_u8(dv[t] * nrm2s) * nrm2s;
+    const float nrm2s = bc[kslot][1];
+    if (lead)
+      for (int t = q; t < kDescLen; t += 8) dv[t] = sat_u8(dv[t] * nrm2s) * nrm2s;
     wave_sync_d();
-    if (q == 0) {
+    if (q == 0 && lead) {
       float nrm1 = 0;
       for (int t = 0; t < kDescLen; ++t) nrm1 = nrm1 + dv[t];
-      bc[g][2] = 1.f / (nrm1 < FLT_EPSILON ? FLT_EPSILON : nrm1);
+      bc[kslot][2] = 1.f / (nrm1 < FLT_EPSILON ? FLT_EPSILON : nrm1);
     }
     wave_sync_d();
-    const float nrm1 = bc[g][2];
-    if (active) {
+    const float nrm1 = bc[kslot][2];
+    if (active && lead) {
       float4* out = reinterpret_cast<float4*>(A.desc + (long long)k * kDescLen) + q * 4;
       const float4* src = reinterpret_cast<const float4*>(dv) + q * 4;
 #pragma unroll
@@ -753,10 +836,16 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                         const sift_keypoint* kpts, const int* img_kp_off, int batch, int kp_cap,
                         float* desc, int first_octave, int* err_flag, bool detected, int* perm) {
   if (kp_cap <= 0) return;
-  // one image of up to kOneImagePx: about one sub-batch per wave, so the
-  // launch lasts as long as its largest window whatever the grouping -- no
-  // ranking pass (8.4 us per 1080p image), keypoints in their own order
-  const bool rank = !(detected && one_image_variants(L, batch));
+  // Every launch ranks (8.4 us per 1080p image).  One image of up to
+  // kOneImagePx splits each window over PARTS groups (row halves) and takes
+  // the parts largest first over the whole launch: round 6, configs[1]'s
+  // descriptor 281 us whole-window (groups of 8, own order), 207 with 4 parts,
+  // 197 + 8 ranked, 182 + 8 with 2 parts ranked; 8 parts 238-262 (1.9 x the
+  // samples); profiles/r6_desc_one_image_ab.txt.
+#ifndef SIFT_DESC_ONE_RANK
+#define SIFT_DESC_ONE_RANK 1  // A/B builds only: 0 = one image in its own order
+#endif
+  const bool rank = !(detected && one_image_variants(L, batch)) || SIFT_DESC_ONE_RANK;
   if (rank)
     hipLaunchKernelGGL(desc_rank_kernel, dim3(std::min((kp_cap + kRankChunk - 1) / kRankChunk, 4096)),
                        dim3(kRankChunk), 0, st, kpts, img_kp_off, batch, kp_cap, perm);
@@ -773,8 +862,9 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
   A.first_octave = first_octave;
   A.err_flag = err_flag;
   // detected keypoints gather two batches ahead (PF = 2): one image of up to
-  // kOneImagePx (one_image_variants) is budgeted for 2 waves per SIMD (few
-  // waves, latency-bound chains), batches and larger images for kDescWpe;
+  // kOneImagePx (one_image_variants) in window parts at 4 waves per SIMD
+  // (2: 223 vs 197 us ranked with 4 parts), batches and larger images whole
+  // at kDescWpe;
   // caller keypoints (calDescriptor: any radius, the whole-window walk) run
   // the general form one batch ahead
 #ifndef SIFT_DESC_GRID_PCT
@@ -785,8 +875,14 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                      dim3(std::max(8, resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192) *     \
                                           SIFT_DESC_GRID_PCT / 800 * 8)),                                           \
                      dim3(64), 0, st, A)
+#ifndef SIFT_DESC_ONE_PARTS
+#define SIFT_DESC_ONE_PARTS 2  // A/B builds only (tools/build_var.sh): 1 = whole windows, 4, 8 parts
+#endif
+#ifndef SIFT_DESC_ONE_WPE
+#define SIFT_DESC_ONE_WPE 4
+#endif
   if (detected && one_image_variants(L, batch))
-    SIFT_DESC_LAUNCH(true, 2, 2);
+    SIFT_DESC_LAUNCH(true, 2, SIFT_DESC_ONE_WPE, SIFT_DESC_ONE_PARTS);
   else if (detected)
     SIFT_DESC_LAUNCH(true, 2, kDescWpe);
   else

@@ -4,7 +4,8 @@
 # the counters), optionally for several library builds; pmc_table.py turns
 # each run into a table.  Replaces pmc_kernel.sh / pmc_lib.sh / pmc_tri.sh.
 # usage: tools/pmc.sh <tag> <kernel regex> [<lib name>...]   (MODE=fast: SIFT_FLAG_FAST;
-#        PMC_SETS=sq|mem|all, default sq)
+#        PMC_SETS=sq|mem|all, default sq; PROG="<script + args>" instead of tools/stage_bench.py,
+#        e.g. PROG="tools/single_trace.py --reps 3" for the one-image kernels)
 set -o pipefail
 TAG=$1; RE=$2; shift 2
 [ -n "$TAG" ] && [ -n "$RE" ] || { sed -n '2,8p' "$0"; exit 2; }
@@ -31,7 +32,7 @@ for n in "$@"; do
   for grp in "${SETS[@]}"; do
     i=$((i+1))
     timeout -k 5 -s KILL 90 rocprofv3 --kernel-trace --pmc $grp -T --kernel-include-regex "$RE" -d $OUT/p$i -o run \
-      --output-format csv -- python3 tools/stage_bench.py --reps 1 --ignore-status $FL > $OUT/p$i.log 2>&1 \
+      --output-format csv -- python3 ${PROG:-tools/stage_bench.py --reps 1 --ignore-status $FL} > $OUT/p$i.log 2>&1 \
       || { echo "pass $n $i failed"; tail -5 $OUT/p$i.log; exit 1; }
   done
   python3 tools/pmc_table.py $OUT > $OUT/table.txt
