@@ -42,7 +42,10 @@ __device__ __forceinline__ void wave_sync() {
 // image is therefore exactly the reference's scan order (src/sift.cpp:556-557,
 // 487-491), which makes the ordered compaction a plain scan over words.
 constexpr int kMaxSeg = 2 * kMaxOctaves;
-constexpr int kWordChunk = 2048;  // mask words per workgroup in the count/expand passes
+#ifndef SIFT_WORD_CHUNK
+#define SIFT_WORD_CHUNK 512  // A/B builds only (tools/build_var.sh); round 6: 2048 -> 512, one image's mask_expand 11.4 -> 4.9 us
+#endif
+constexpr int kWordChunk = SIFT_WORD_CHUNK;  // mask words per workgroup in the count/expand passes
 
 struct MaskLayout {
   int n;                          // segments = n_oct * 2
@@ -334,9 +337,17 @@ __global__ __launch_bounds__(256) void mask_expand_kernel(MaskLayout M, const un
   const long long base = (long long)blockIdx.x * kWordChunk;
   const unsigned* m = mask + b * M.w_img;
   int run = blk_off[b * M.bpw + blockIdx.x];
+  // every word of the chunk in flight at once (the loop below synchronises per step)
+  unsigned words[kWordChunk / 256];
+#pragma unroll
   for (int it = 0; it < kWordChunk / 256; ++it) {
     const long long w = base + it * 256 + threadIdx.x;
-    unsigned bits = w < M.w_img ? m[w] : 0u;
+    words[it] = w < M.w_img ? m[w] : 0u;
+  }
+#pragma unroll
+  for (int it = 0; it < kWordChunk / 256; ++it) {
+    const long long w = base + it * 256 + threadIdx.x;
+    unsigned bits = words[it];
     const int cnt = __popc(bits);
     int incl = cnt;
     for (int off = 1; off < 64; off <<= 1) {
@@ -477,7 +488,7 @@ __global__ __launch_bounds__(kScanT) void scan_down_kernel(const int* __restrict
 // The same exclusive scan in one workgroup for short lists (one image's
 // candidate blocks and orientation peaks): one launch instead of three, on a
 // path whose launches are latency-bound.  Thread t owns the `per` consecutive
-// elements [t * per, t * per + per); out[n] = total.
+// elements [t * per, t * per + per) (per <= 64, in registers); out[n] = total.
 // Per-image offsets from a scan: gout[b] = out[b * stride] (idx == nullptr) or
 // out[min(idx[b], n)], b = 0..batch (gather_offsets_kernel's contract).
 struct ScanGather {
@@ -493,10 +504,29 @@ __global__ __launch_bounds__(1024) void scan_small_kernel(const int* __restrict_
   __shared__ int wsum[16];
   const int n = scan_n(n_dev, n_host, cap);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int per = (n + 1023) / 1024;
+  // a multiple of 4 (<= kScanSmallMax / 1024): the chunk is read as int4s, all
+  // in flight at once -- a loop of dependent loads cost ~13 us for a 1080p
+  // image's ~50 K candidates (round 6)
+  const int per = ((n + 1023) / 1024 + 3) & ~3;
   const int i0 = tid * per;
+  const bool vec = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  int v[kScanSmallMax / 1024];
+#pragma unroll
+  for (int k = 0; k < kScanSmallMax / 1024; k += 4) {
+    if (k < per && vec && i0 + k + 3 < n) {
+      const int4 q = *reinterpret_cast<const int4*>(in + i0 + k);
+      v[k] = q.x;
+      v[k + 1] = q.y;
+      v[k + 2] = q.z;
+      v[k + 3] = q.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[k + u] = k < per && i0 + k + u < n ? in[i0 + k + u] : 0;
+    }
+  }
   int s = 0;
-  for (int k = 0; k < per; ++k) s += i0 + k < n ? in[i0 + k] : 0;
+#pragma unroll
+  for (int k = 0; k < kScanSmallMax / 1024; ++k) s += v[k];
   int incl = s;
   for (int off = 1; off < 64; off <<= 1) {
     const int t = __shfl_up(incl, off);
@@ -509,10 +539,11 @@ __global__ __launch_bounds__(1024) void scan_small_kernel(const int* __restrict_
     run += k < wv ? wsum[k] : 0;
     tot += wsum[k];
   }
-  for (int k = 0; k < per; ++k)
-    if (i0 + k < n) {
+#pragma unroll
+  for (int k = 0; k < kScanSmallMax / 1024; ++k)
+    if (k < per && i0 + k < n) {
       out[i0 + k] = run;
-      run += in[i0 + k];
+      run += v[k];
     }
   if (tid == 0) {
     out[n] = tot;

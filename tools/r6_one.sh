@@ -1,7 +1,7 @@
 #!/bin/bash
 # One-image (configs[1]) kernel times per library build: rocprofv3 --kernel-trace
 # --stats over tools/single_trace.py, top kernels by total time, then SQ
-# counters of the descriptor kernels (tools/pmc.sh with PROG).
+# counters (PMC=1) of the kernels matching PMC_RE, default "descriptor" (tools/pmc.sh with PROG).
 # usage: tools/r6_one.sh <tag> <variant>...   (variant: cur | lib/libsift_hip_<name>.so)
 set -o pipefail
 export TMPDIR=/tmp
@@ -23,5 +23,5 @@ for r in rows[:6]:
 PY
 done
 cp $L/libsift_hip_keep1.so $L/libsift_hip.so
-[ -n "$PMC" ] && PROG="tools/single_trace.py --reps 3" bash tools/pmc.sh one_$TAG "descriptor" "$@"
+[ -n "$PMC" ] && PROG="tools/single_trace.py --reps 3" bash tools/pmc.sh one_$TAG "${PMC_RE:-descriptor}" "$@"
 exit 0
