@@ -298,24 +298,38 @@ void launch_blur_octave(hipStream_t st, const Layout& L, int o, float* gpyr, con
 // issues at full rate, an SGPR one at half); the window is 19 ds_read_b64 per
 // row for w = 18 (row pitch 96 = 32 mod 64 words: the two tile rows of a
 // 32-lane pass fill opposite bank halves, conflict free).
-constexpr int kSW = 32, kSH = 16, kSLP = 96;
+// PX = 4 (round 6; a launch of >= kSmall4Min workgroups: one 1080p image's
+// octave 1): 4 outputs per lane of a 64 x 16 tile, the window as ds_read_b128
+// (row pitch 128 words: a 16-lane group's reads cover 64 distinct banks), so
+// a kernel row costs 20 LDS reads per 296 VALU instead of 29 per 148 -- the
+// 2-output form was LDS-issue-bound there (SQ_WAIT_INST_LDS 0.40 of the wave
+// cycles, VALU issue 0.52).
+constexpr int kSH = 16;
+#ifndef SIFT_SMALL4_MIN
+#define SIFT_SMALL4_MIN 1024  // A/B builds only (tools/build_var.sh)
+#endif
+constexpr long long kSmall4Min = SIFT_SMALL4_MIN;
 
-template <int W>
+template <int W, int PX = 2>
 struct SmallTile {
+  static constexpr int SW = 16 * PX;            // tile width
+  static constexpr int SLP = PX == 4 ? 128 : 96;  // LDS row pitch (words)
   static constexpr int KS = 2 * W + 1;
   static constexpr int KP = (KS + 3) / 4 * 4;  // coefficient row pitch (b128 reads)
-  static constexpr int LR = kSH + 2 * W, LW = kSW + 2 * W;
-  static constexpr int LDS_FLOATS = LR * kSLP + KS * KP;
-  static_assert(LW <= kSLP, "row pitch");
+  static constexpr int NW = (KS + PX - 1 + PX - 1) / PX * PX;  // window values a lane reads per row
+  static constexpr int LR = kSH + 2 * W, LW = SW + 2 * W;
+  static constexpr int LDS_FLOATS = LR * SLP + KS * KP;
+  static_assert(LW <= SLP && PX * 15 + NW <= LW, "row pitch / window reads inside the staged row");
 };
 
-template <int W>
+template <int W, int PX = 2>
 __device__ __forceinline__ void blur_small_tile(const float* __restrict__ src, long long spitch, int rows, int cols,
                                                 float* __restrict__ dst, long long dpitch,
                                                 const float* __restrict__ coef, int x0, int y0,
                                                 float* __restrict__ lds,
                                                 NextPlane nx = NextPlane{nullptr, 0, 0, 0}) {
-  using T = SmallTile<W>;
+  using T = SmallTile<W, PX>;
+  constexpr int kSLP = T::SLP;
   const int t = threadIdx.x;
   float* kt = lds + T::LR * kSLP;
   for (int i = t; i < T::KS * T::KS; i += 256) {
@@ -330,7 +344,9 @@ __device__ __forceinline__ void blur_small_tile(const float* __restrict__ src, l
   }
   __syncthreads();
   const int tx = t & 15, ty = t >> 4;
-  float acc0 = 0.f, acc1 = 0.f;
+  float acc[PX];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) acc[i] = 0.f;
 #pragma unroll 1
   for (int a = 0; a < T::KS; ++a) {
     float k[T::KP];
@@ -343,32 +359,51 @@ __device__ __forceinline__ void blur_small_tile(const float* __restrict__ src, l
       k[4 * q + 2] = v.z;
       k[4 * q + 3] = v.w;
     }
-    float win[T::KS + 1];
-    const float2* w2 = reinterpret_cast<const float2*>(lds + (ty + a) * kSLP + 2 * tx);
+    float win[T::NW];
+    if constexpr (PX == 4) {
+      const float4* w4 = reinterpret_cast<const float4*>(lds + (ty + a) * kSLP + 4 * tx);
 #pragma unroll
-    for (int q = 0; q < (T::KS + 1) / 2; ++q) {
-      const float2 v = w2[q];
-      win[2 * q] = v.x;
-      win[2 * q + 1] = v.y;
+      for (int q = 0; q < T::NW / 4; ++q) {
+        const float4 v = w4[q];
+        win[4 * q] = v.x;
+        win[4 * q + 1] = v.y;
+        win[4 * q + 2] = v.z;
+        win[4 * q + 3] = v.w;
+      }
+    } else {
+      const float2* w2 = reinterpret_cast<const float2*>(lds + (ty + a) * kSLP + 2 * tx);
+#pragma unroll
+      for (int q = 0; q < T::NW / 2; ++q) {
+        const float2 v = w2[q];
+        win[2 * q] = v.x;
+        win[2 * q + 1] = v.y;
+      }
     }
 #pragma unroll
     for (int b = 0; b < T::KS; ++b) {
-      const float p0 = win[b] * k[b], p1 = win[b + 1] * k[b];
-      acc0 = acc0 + p0;
-      acc1 = acc1 + p1;
+      float p[PX];
+#pragma unroll
+      for (int i = 0; i < PX; ++i) p[i] = win[b + i] * k[b];
+#pragma unroll
+      for (int i = 0; i < PX; ++i) acc[i] = acc[i] + p[i];
     }
   }
-  const int y = y0 + ty, x = x0 + 2 * tx;
+  const int y = y0 + ty, x = x0 + PX * tx;
   if (y < rows) {
     float* drow = dst + (long long)y * dpitch + x;
-    if (x < cols) drow[0] = acc0 / 8192.f;
-    if (x + 1 < cols) drow[1] = acc1 / 8192.f;
-    // x is even: output 0 -> next plane (y/2, x/2) on even rows
-    if (nx.p && (y & 1) == 0 && (y >> 1) < nx.rows && (x >> 1) < nx.cols)
-      nx.p[(long long)(y >> 1) * nx.pitch + (x >> 1)] = acc0 / 8192.f;
+#pragma unroll
+    for (int i = 0; i < PX; ++i)
+      if (x + i < cols) drow[i] = acc[i] / 8192.f;
+    // x is even: outputs 0 (and 2) -> next plane (y/2, x/2 (+1)) on even rows
+    if (nx.p && (y & 1) == 0 && (y >> 1) < nx.rows) {
+#pragma unroll
+      for (int i = 0; i < PX; i += 2)
+        if (((x + i) >> 1) < nx.cols) nx.p[(long long)(y >> 1) * nx.pitch + ((x + i) >> 1)] = acc[i] / 8192.f;
+    }
   }
 }
 
+template <int PX>
 __global__ __launch_bounds__(256) void blur_small_kernel(OctaveArgs A) {
   extern __shared__ float4 lds4[];
   float* lds = reinterpret_cast<float*>(lds4);
@@ -377,14 +412,14 @@ __global__ __launch_bounds__(256) void blur_small_kernel(OctaveArgs A) {
   const int si = 3 - (z & 3);  // heaviest scale first
   const float* src = A.gpyr + b * A.g_img + A.base_off;
   float* dst = A.gpyr + b * A.g_img + A.dst_off[si];
-  const int x0 = blockIdx.x * kSW, y0 = blockIdx.y * kSH;
+  const int x0 = blockIdx.x * SmallTile<4, PX>::SW, y0 = blockIdx.y * kSH;
   NextPlane nx = A.nx;
   if (nx.p) nx.p += b * A.g_img;
   switch (si) {
-    case 0: blur_small_tile<4>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[0], x0, y0, lds); break;
-    case 1: blur_small_tile<8>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[1], x0, y0, lds, nx); break;
-    case 2: blur_small_tile<12>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[2], x0, y0, lds); break;
-    default: blur_small_tile<18>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[3], x0, y0, lds); break;
+    case 0: blur_small_tile<4, PX>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[0], x0, y0, lds); break;
+    case 1: blur_small_tile<8, PX>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[1], x0, y0, lds, nx); break;
+    case 2: blur_small_tile<12, PX>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[2], x0, y0, lds); break;
+    default: blur_small_tile<18, PX>(src, A.pitch, A.rows, A.cols, dst, A.pitch, A.coef[3], x0, y0, lds); break;
   }
 }
 
@@ -412,8 +447,14 @@ void launch_blur_octave_small(hipStream_t st, const Layout& L, int o, float* gpy
   A.cols = O.cols;
   A.pad_ = 0;
   A.nx = next_plane(L, o, gpyr, fuse_next);
-  dim3 grid((O.cols + kSW - 1) / kSW, (O.rows + kSH - 1) / kSH, batch * 4);
-  hipLaunchKernelGGL(blur_small_kernel, grid, dim3(256), SmallTile<18>::LDS_FLOATS * 4, st, A);
+  const int rt = (O.rows + kSH - 1) / kSH;
+  const long long wg4 = (long long)((O.cols + SmallTile<4, 4>::SW - 1) / SmallTile<4, 4>::SW) * rt * batch * 4;
+  constexpr size_t lds4 = SmallTile<18, 4>::LDS_FLOATS * 4, lds2 = SmallTile<18, 2>::LDS_FLOATS * 4;
+  constexpr int sw4 = SmallTile<4, 4>::SW, sw2 = SmallTile<4, 2>::SW;
+  if (wg4 >= kSmall4Min)
+    hipLaunchKernelGGL(blur_small_kernel<4>, dim3((O.cols + sw4 - 1) / sw4, rt, batch * 4), dim3(256), lds4, st, A);
+  else
+    hipLaunchKernelGGL(blur_small_kernel<2>, dim3((O.cols + sw2 - 1) / sw2, rt, batch * 4), dim3(256), lds2, st, A);
 }
 
 // ---- exact 2-D blur, symmetric scatter form (the SIFT_NCL tables) ----------
