@@ -81,7 +81,7 @@ struct DescArgs {
 // inv_a = 1 / a (per keypoint): the bounds only have to enclose the samples
 // the exact predicate keeps, and the margin (>= 0.057 in j for |a| <= 1/5.7)
 // dwarfs the rounding of a multiply by the reciprocal.
-// A window part (PARTS = 4, below) narrows |.| < 2.5 to (lim_lo, lim_hi).
+// A window part (PARTS > 1, below) narrows |.| < 2.5 to (lim_lo, lim_hi).
 __device__ __forceinline__ void slab(float a, float inv_a, float b, int& lo, int& hi, float lim_lo = -2.5f,
                                      float lim_hi = 2.5f) {
   const float m = 1e-2f;  // margin >> float rounding of r_rot / c_rot
@@ -129,9 +129,9 @@ struct RecT {  // one lane's 8 corner records
 // (profiles/r4_desc_pf2_ab.txt; three batches ahead, 38 spills: 5.56-5.58 vs
 // 5.50-5.51, round 5).  WPE: waves per SIMD the registers are budgeted for
 // (PF = 2 at 4: 128 VGPRs, the spills outside the sample loop).
-// PARTS = 4 (one image, round 6): a keypoint's window is split over four
-// groups of one wave by the half of the interior rows and columns its bins lie
-// in; see "Window parts" below.
+// PARTS = 2 (one image, round 6; 4 and 8 for A/B builds): a keypoint's window
+// is split over PARTS groups of one wave by the part of the interior rows (and
+// columns) its bins lie in; see "Window parts" below.
 template <bool DET, int PF, int WPE, int PARTS = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 descriptor_kernel(DescArgs A) {
@@ -188,8 +188,10 @@ descriptor_kernel(DescArgs A) {
         const int clen = min(kRankChunk, n - c * kRankChunk), r = clen - 1 - (j * kKpw + lane);
         if (lane < kKpw) sord[lane] = r >= 0 ? A.perm[c * kRankChunk + r] : kend;
       } else {
+        // unranked: last keypoint first -- within an octave the keypoints come
+        // in layer order and a layer's windows are larger than the one before
         const int i = sb * kKpw + lane;
-        if (lane < kKpw) sord[lane] = i < kend ? i : kend;
+        if (lane < kKpw) sord[lane] = i < kend ? kend - 1 - i : kend;
       }
       wave_sync_d();
     } else {
@@ -201,18 +203,17 @@ descriptor_kernel(DescArgs A) {
     }
     const int kslot = g / PARTS;            // this group's keypoint among the wave's kKpw
     const bool lead = g % PARTS == 0;       // the group that normalises and stores it
-    // Window parts (PARTS = 4): part (hr, hc) of a keypoint owns the interior
-    // bins with R >> 1 == hr and C >> 1 == hc.  A sample reaches them only
-    // from base corners Rm in [2 hr - 1, 2 hr + 1] -- rbin in [2 hr - 1,
-    // 2 hr + 2), r_rot in [2 hr - 2.5, 2 hr + 0.5) -- likewise for columns, so
-    // the part walks the samples of that sub-square (slab limits below, ~36 %
-    // of the window), in raster order, and masks the corners outside its
-    // bins like those outside the interior: each of its bins sums the same
-    // samples in the same order as a whole-window walk, and a keypoint's
-    // longest chain is ~0.36 of the window's.
-    // (PARTS = 8: part (rq, hc) owns the row R == rq alone: Rm in {rq - 1, rq},
-    // r_rot in [rq - 2.5, rq - 0.5))
-    // (PARTS = 2: part hr owns the row half alone, all columns)
+    // Window parts (PARTS = 2): part hr of a keypoint owns the interior bins
+    // with R >> 1 == hr.  A sample reaches them only from base corners Rm in
+    // [2 hr - 1, 2 hr + 1] -- rbin in [2 hr - 1, 2 hr + 2), r_rot in
+    // [2 hr - 2.5, 2 hr + 0.5) -- so the part walks the samples of that band
+    // (slab limits below, ~60 % of the window), in raster order, and masks the
+    // corners outside its bins like those outside the interior: each of its
+    // bins sums the same samples in the same order as a whole-window walk,
+    // and a keypoint's longest chain is ~0.6 of the window's.
+    // (PARTS = 4: part (hr, hc) also halves the columns the same way, ~36 %;
+    // PARTS = 8: part (rq, hc) owns the row R == rq alone: Rm in {rq - 1, rq},
+    // r_rot in [rq - 2.5, rq - 0.5).)
     const int hr = PARTS == 4 ? (g >> 1) & 1 : PARTS == 2 ? g & 1 : 0, hc = PARTS >= 4 ? g & 1 : 0;
     const int rq = PARTS == 8 ? g >> 1 : 0;
     const float rlim_lo = PARTS == 8 ? rq - 2.5f : PARTS > 1 ? 2.f * hr - 2.5f : -2.5f;
@@ -836,14 +837,15 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                         const sift_keypoint* kpts, const int* img_kp_off, int batch, int kp_cap,
                         float* desc, int first_octave, int* err_flag, bool detected, int* perm) {
   if (kp_cap <= 0) return;
-  // Every launch ranks (8.4 us per 1080p image).  One image of up to
-  // kOneImagePx splits each window over PARTS groups (row halves) and takes
-  // the parts largest first over the whole launch: round 6, configs[1]'s
-  // descriptor 281 us whole-window (groups of 8, own order), 207 with 4 parts,
-  // 197 + 8 ranked, 182 + 8 with 2 parts ranked; 8 parts 238-262 (1.9 x the
-  // samples); profiles/r6_desc_one_image_ab.txt.
+  // One image of up to kOneImagePx splits each window over PARTS groups (row
+  // halves) and takes its keypoints last first (a layer's windows are larger
+  // than the previous layer's), no ranking pass (8.4 us per 1080p image):
+  // round 6, configs[1]'s descriptor 281 us whole-window (groups of 8, own
+  // order), 207 with 4 parts, 197 + 8 ranked largest first, 182-192 + 8 with 2
+  // parts ranked, 194 with 2 parts last first (217 first first); 8 parts
+  // 238-262 (1.9 x the samples); profiles/r6_desc_one_image_ab.txt.
 #ifndef SIFT_DESC_ONE_RANK
-#define SIFT_DESC_ONE_RANK 1  // A/B builds only: 0 = one image in its own order
+#define SIFT_DESC_ONE_RANK 0  // A/B builds only: 1 = rank one image too (largest first)
 #endif
   const bool rank = !(detected && one_image_variants(L, batch)) || SIFT_DESC_ONE_RANK;
   if (rank)
