@@ -20,14 +20,18 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--flags", type=int, default=0)
+    p.add_argument("--rows", type=int, default=1080)
+    p.add_argument("--cols", type=int, default=1920)
+    p.add_argument("--octaves", type=int, default=4)
+    p.add_argument("--cap", type=int, default=40000)
     a = p.parse_args()
-    R, C = 1080, 1920
+    R, C = a.rows, a.cols
     with siftgpu.Context(R, C, 1, device=0) as ctx:
-        ctx.set_octaves(4)
+        ctx.set_octaves(a.octaves)
         ctx.set_flags(a.flags)
         img = torch.empty((1, R, C), dtype=torch.float32, device="cuda")
         ctx.synth_images(img.data_ptr(), 1, R, C, C, R * C, seed_base=0)
-        cap = 40000
+        cap = a.cap
         kpts = torch.empty((cap, 7), dtype=torch.int32, device="cuda")
         desc = torch.empty((cap, 128), dtype=torch.float32, device="cuda")
         offs = torch.empty((2,), dtype=torch.int32, device="cuda")
