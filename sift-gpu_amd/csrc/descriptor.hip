@@ -850,7 +850,21 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                      dim3(std::max(8, resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192) *     \
                                           SIFT_DESC_GRID_PCT / 800 * 8)),                                           \
                      dim3(64), 0, st, A)
-  if (detected && one_image_variants(L, batch))
+#ifndef SIFT_DESC_ONE_GRID
+#define SIFT_DESC_ONE_GRID 1  // A/B builds only (tools/build_var.sh): 0 = the resident grid
+#endif
+  if (detected && one_image_variants(L, batch) && SIFT_DESC_ONE_GRID)
+    // a workgroup per sub-batch of the capacity (waves past the keypoint count
+    // exit at once): the dispatcher hands the next sub-batch to whichever wave
+    // slot frees first, as for the one-image orientation (192 vs 201 us per
+    // 1080p image, round 6)
+    // (at most 4 resident grids: a large capacity does not launch empty waves
+    // without bound; the kernel strides past its grid)
+    hipLaunchKernelGGL((descriptor_kernel<true, 2, kDescWpe, 2>),
+                       dim3(std::min((kp_cap + 3) / 4,
+                                     4 * resident_grid((const void*)descriptor_kernel<true, 2, kDescWpe, 2>, 64, 0, 8192))),
+                       dim3(64), 0, st, A);
+  else if (detected && one_image_variants(L, batch))
     SIFT_DESC_LAUNCH(true, 2, kDescWpe, 2);
   else if (detected)
     SIFT_DESC_LAUNCH(true, 2, kDescWpe);

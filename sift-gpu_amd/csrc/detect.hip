@@ -649,12 +649,15 @@ void launch_extrema(hipStream_t st, const Layout& L, const float* gpyr, float* d
   W.mc = mc;
   W.mask = D.mask;
   // rows per wave: about 64 K waves over the launch (measured on the
-  // 64 x 1080p batch: 16 K 1.70 ms, 32 K 1.60, 64 K 1.56), at least 8 rows
-  // (a chunk re-reads 2 rows)
+  // 64 x 1080p batch: 16 K 1.70 ms, 32 K 1.60, 64 K 1.56), at least
+  // SIFT_EXTREMA_MIN_CHUNK rows (a chunk re-reads 2 rows)
   long long strip_rows = 0;
   for (int o = 0; o < L.n_oct; ++o) strip_rows += (long long)((L.oct[o].cols + 63) / 64) * L.oct[o].rows;
   constexpr long long target = 65536;  // waves per launch (16 K / 32 K / 64 K measured in round 2)
-  W.chunk = (int)std::min<long long>(512, std::max<long long>(8, strip_rows * batch / target));
+#ifndef SIFT_EXTREMA_MIN_CHUNK
+#define SIFT_EXTREMA_MIN_CHUNK 4  // A/B builds only (tools/build_var.sh); one 1080p image: 4 rows 28.9 us, 8 30.7 (round 6)
+#endif
+  W.chunk = (int)std::min<long long>(512, std::max<long long>(SIFT_EXTREMA_MIN_CHUNK, strip_rows * batch / target));
   int w = 0;
   for (int o = 0; o < L.n_oct; ++o) {
     W.wave_start[o] = w;
@@ -899,8 +902,12 @@ __device__ __forceinline__ int ori_radius(float size, int o) {
 // (A per-XCD dynamic candidate fetch was bit-exact and 16 % slower: each
 // draw is a returning atomic that sits in vmcnt order ahead of the
 // candidate's gathers; tools/patches/r5_variants.patch.)
-constexpr int kOBW = 4;  // waves per workgroup
+[[maybe_unused]] constexpr int kOBWaves = 4;  // waves per workgroup (persistent form, SIFT_ORIENT_PERSIST)
 
+// PERSIST = false (A/B): one wave per candidate over a grid of the candidate
+// capacity, one wave per workgroup -- the dispatcher hands the next candidate
+// to whichever slot frees, instead of a fixed stride per resident wave.
+template <int kOBW, bool PERSIST>
 __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   __shared__ float vals[kOBW][64][kOriBins];  // [wave][rank][bin]: owner reads are conflict free
   __shared__ int cnt[kOBW][64];
@@ -914,11 +921,12 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   cnt[w][lane] = 0;
   // XCD-aware contiguous split of the raster-ordered candidates (speed only):
   // XCD x takes [x per, (x + 1) per), its waves interleaved over them
-  const int nw = (int)(gridDim.x >> 3) * kOBW;
+  const int nw = PERSIST ? (int)(gridDim.x >> 3) * kOBW : 1;
   const int per = (n + 7) / 8;
   const int xcd = blockIdx.x & 7, wid = (int)(blockIdx.x >> 3) * kOBW + w;
-  const int c0 = xcd * per, cend = min(n, c0 + per);
-  for (int ci = c0 + wid; ci < cend; ci += nw) {
+  const int c0 = PERSIST ? xcd * per : (int)blockIdx.x * kOBW + w;
+  const int cend = PERSIST ? min(n, c0 + per) : min(n, c0 + 1);
+  for (int ci = PERSIST ? c0 + wid : c0; ci < cend; ci += nw) {
     const CandOut& co = A.couts[ci];
     if (co.npeaks == 0) {  // refinement rejected it
       if (lane == 0) A.npeaks[ci] = 0;
@@ -1323,10 +1331,23 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
   // is a window's largest per-batch bin counts instead of its whole sample
   // walk.  Every variant is bit-identical (the losers are kept as
   // tools/patches/r5_variants.patch).
-  if (one_image_variants(L, batch))
-    hipLaunchKernelGGL(orient_bin_kernel, dim3(resident_grid((const void*)orient_bin_kernel, 64 * kOBW, 0, 2048)),
-                       dim3(64 * kOBW), 0, st, A);
-  else
+  // One image: a workgroup (one wave) per candidate slot, so the dispatcher
+  // gives the next candidate to whichever wave slot frees first -- a fixed
+  // stride per resident wave left the waves alive 40 % of the launch on
+  // average (61.6 vs 41.8 us for one 1080p image, round 6; rejected
+  // candidates exit after one load).
+#ifndef SIFT_ORIENT_PERSIST
+#define SIFT_ORIENT_PERSIST 0  // A/B builds only (tools/build_var.sh): 1 = the round-4 resident grid
+#endif
+  if (one_image_variants(L, batch)) {
+#if SIFT_ORIENT_PERSIST
+    hipLaunchKernelGGL((orient_bin_kernel<kOBWaves, true>),
+                       dim3(resident_grid((const void*)orient_bin_kernel<kOBWaves, true>, 64 * kOBWaves, 0, 2048)),
+                       dim3(64 * kOBWaves), 0, st, A);
+#else
+    hipLaunchKernelGGL((orient_bin_kernel<1, false>), dim3(std::max(1, D.cand_cap)), dim3(64), 0, st, A);
+#endif
+  } else
     hipLaunchKernelGGL(orient_slots_kernel<2>,
                        dim3(resident_grid((const void*)orient_slots_kernel<2>, 64, 0, 8192)), dim3(64), 0, st, A);
 }
