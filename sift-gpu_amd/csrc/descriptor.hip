@@ -850,6 +850,9 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                      dim3(std::max(8, resident_grid((const void*)descriptor_kernel<__VA_ARGS__>, 64, 0, 8192) *     \
                                           SIFT_DESC_GRID_PCT / 800 * 8)),                                           \
                      dim3(64), 0, st, A)
+#ifndef SIFT_ONE_BIG_GRIDS
+#define SIFT_ONE_BIG_GRIDS 4  // A/B builds only (tools/build_var.sh); one 8K image: 1 1994 us, 4 1850, 16 1877 (round 6)
+#endif
 #ifndef SIFT_DESC_ONE_GRID
 #define SIFT_DESC_ONE_GRID 1  // A/B builds only (tools/build_var.sh): 0 = the resident grid
 #endif
@@ -866,6 +869,14 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                        dim3(64), 0, st, A);
   else if (detected && one_image_variants(L, batch))
     SIFT_DESC_LAUNCH(true, 2, kDescWpe, 2);
+  else if (detected && batch == 1)
+    // one image above kOneImagePx: several resident grids, so that the slots
+    // that finish early take the remaining strides (the XCD mapping above
+    // works for any grid of whole XCD runs)
+    hipLaunchKernelGGL((descriptor_kernel<true, 2, kDescWpe>),
+                       dim3(resident_grid((const void*)descriptor_kernel<true, 2, kDescWpe>, 64, 0, 8192) *
+                            SIFT_ONE_BIG_GRIDS),
+                       dim3(64), 0, st, A);
   else if (detected)
     SIFT_DESC_LAUNCH(true, 2, kDescWpe);
   else

@@ -1347,9 +1347,12 @@ void launch_refine_orient(hipStream_t st, const Layout& L, const float* gpyr, co
 #else
     hipLaunchKernelGGL((orient_bin_kernel<1, false>), dim3(std::max(1, D.cand_cap)), dim3(64), 0, st, A);
 #endif
-  } else
+  } else {
+    // (one 8K image: 4 resident grids were 457 -> 520 us here, unlike the
+    // descriptor's; profiles/r6_one_image_grids_ab.txt)
     hipLaunchKernelGGL(orient_slots_kernel<2>,
                        dim3(resident_grid((const void*)orient_slots_kernel<2>, 64, 0, 8192)), dim3(64), 0, st, A);
+  }
 }
 
 // ---- ordered keypoint emission ------------------------------------------------
