@@ -68,7 +68,7 @@ struct DescArgs {
   const MathConsts* mc;
   const sift_keypoint* kpts;
   const int* perm;        // [n] keypoint indices ranked by window size within chunks of kRankChunk
-                          // (null: the keypoints' own order, one image)
+                          // (null: one image, last keypoint first -- see the sub-batch loop)
   const int* img_kp_off;  // [batch+1]
   int batch;
   int kp_cap;

@@ -904,9 +904,11 @@ __device__ __forceinline__ int ori_radius(float size, int o) {
 // candidate's gathers; tools/patches/r5_variants.patch.)
 [[maybe_unused]] constexpr int kOBWaves = 4;  // waves per workgroup (persistent form, SIFT_ORIENT_PERSIST)
 
-// PERSIST = false (A/B): one wave per candidate over a grid of the candidate
-// capacity, one wave per workgroup -- the dispatcher hands the next candidate
-// to whichever slot frees, instead of a fixed stride per resident wave.
+// PERSIST = false (the shipped form, round 6): one wave per candidate slot
+// over a grid of the candidate capacity, one wave per workgroup -- the
+// dispatcher hands the next candidate to whichever slot frees, instead of a
+// fixed stride per resident wave (PERSIST = true, kOBW waves per workgroup:
+// round 4's form, an A/B build, SIFT_ORIENT_PERSIST).
 template <int kOBW, bool PERSIST>
 __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   __shared__ float vals[kOBW][64][kOriBins];  // [wave][rank][bin]: owner reads are conflict free
@@ -919,8 +921,9 @@ __global__ __launch_bounds__(64 * kOBW) void orient_bin_kernel(RefArgs A) {
   const float etab_lane = A.mc->exptab[lane];
   const unsigned long long below = (1ull << lane) - 1ull;
   cnt[w][lane] = 0;
-  // XCD-aware contiguous split of the raster-ordered candidates (speed only):
-  // XCD x takes [x per, (x + 1) per), its waves interleaved over them
+  // (PERSIST) XCD-aware contiguous split of the raster-ordered candidates
+  // (speed only): XCD x takes [x per, (x + 1) per), its waves interleaved
+  // over them
   const int nw = PERSIST ? (int)(gridDim.x >> 3) * kOBW : 1;
   const int per = (n + 7) / 8;
   const int xcd = blockIdx.x & 7, wid = (int)(blockIdx.x >> 3) * kOBW + w;
