@@ -21,10 +21,11 @@
 //    bins the fold reads; a border-bin update carries +0.0 into an interior
 //    bin), so all 64 lanes of an update hit distinct banks and a wave needs
 //    5.1 KB, not 11.5 KB.
-//  * One image (round 6): a keypoint's window is split over 2 groups by the
-//    half of the interior rows its bins lie in (window parts, PARTS); each
-//    group walks only the samples that reach its bins, in raster order, so a
-//    keypoint's longest owner chain is ~0.6 of its window.  (Plain LDS
+//  * One image (round 6): a keypoint's window is split over 4 groups by the
+//    half of the interior rows and the half of the interior columns its bins
+//    lie in (window parts, PARTS); each group walks only the samples that
+//    reach its bins, in raster order, so a keypoint's longest owner chain is
+//    ~0.36 of its window.  (Plain LDS
 //    read-modify-writes: ds_add_f32 is bit-exact here but took the batch
 //    descriptor from 5.6 to 50.9 ms; profiles/r6_desc_one_image_ab.txt.)
 //  * Fold, 0.2 clamp, uchar quantisation, RootSIFT (src/sift.cpp:676-721)
@@ -129,15 +130,14 @@ struct RecT {  // one lane's 8 corner records
 // (profiles/r4_desc_pf2_ab.txt; three batches ahead, 38 spills: 5.56-5.58 vs
 // 5.50-5.51, round 5).  WPE: waves per SIMD the registers are budgeted for
 // (PF = 2 at 4: 128 VGPRs, the spills outside the sample loop).
-// PARTS = 2 (one image, round 6): a keypoint's window is split over two
-// groups of one wave by the half of the interior rows its bins lie in; see
-// "Window parts" below.  (4 and 8 parts, and ranked orders for them:
-// tools/patches/desc_parts48.patch.)
+// PARTS = 4 (one image, round 6; 2 and 8 for A/B builds): a keypoint's window
+// is split over PARTS groups of one wave by the part of the interior rows (and
+// columns) its bins lie in; see "Window parts" below.
 template <bool DET, int PF, int WPE, int PARTS = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 descriptor_kernel(DescArgs A) {
   static_assert(PF == 1 || PF == 2, "one or two sample batches in flight");
-  static_assert(PARTS == 1 || (PARTS == 2 && DET), "window parts: detected keypoints (row table) only");
+  static_assert(PARTS == 1 || ((PARTS == 2 || PARTS == 4 || PARTS == 8) && DET), "window parts: detected keypoints (row table) only");
   constexpr int kKpw = kGrp / PARTS;  // keypoints per wave
   // [qidx][group*8 + parity]
   constexpr int kHistRows = kQBins;
@@ -173,18 +173,27 @@ descriptor_kernel(DescArgs A) {
   // per-chunk XOR by c itself repeats every two passes at 16 chunks a pass:
   // 6.31 vs 5.85 ms, the waves alive 72 % of the launch instead of 79 %).
   // Keypoints are independent; only the processing order changes.
-  // (PARTS > 1: one image, unranked, kKpw keypoints per wave)
+  // (PARTS > 1: one image, kKpw keypoints per wave, last first or ranked)
   const int per = ((n + 7) / 8 + kRankChunk - 1) / kRankChunk * kRankChunk;
   const int k0 = PARTS > 1 ? 0 : xcd * per;
   const int kend = PARTS > 1 ? n : min(n, (xcd + 1) * per);
-  const int nsb = PARTS > 1 ? (n + kKpw - 1) / kKpw
+  const int nch = (n + kRankChunk - 1) / kRankChunk;
+  const int nsb = PARTS > 1 ? (A.perm ? nch * (kRankChunk / kKpw) : (n + kKpw - 1) / kKpw)
                             : (max(kend - k0, 0) + kRankChunk - 1) / kRankChunk * kSubPerChunk;
   for (int sb = PARTS > 1 ? (int)blockIdx.x : slot; sb < nsb; sb += PARTS > 1 ? (int)gridDim.x : nslot) {
     if constexpr (PARTS > 1) {
-      // last keypoint first: within an octave the keypoints come in layer
-      // order and a layer's windows are larger than the one before
-      const int i = sb * kKpw + lane;
-      if (lane < kKpw) sord[lane] = i < kend ? kend - 1 - i : kend;
+      if (A.perm) {
+        // largest windows first over the whole launch: sub-batch sb takes ranks
+        // kKpw j .. from the top of chunk sb % nch (j = sb / nch)
+        const int c = sb % nch, j = sb / nch;
+        const int clen = min(kRankChunk, n - c * kRankChunk), r = clen - 1 - (j * kKpw + lane);
+        if (lane < kKpw) sord[lane] = r >= 0 ? A.perm[c * kRankChunk + r] : kend;
+      } else {
+        // unranked: last keypoint first -- within an octave the keypoints come
+        // in layer order and a layer's windows are larger than the one before
+        const int i = sb * kKpw + lane;
+        if (lane < kKpw) sord[lane] = i < kend ? kend - 1 - i : kend;
+      }
       wave_sync_d();
     } else {
       const int ch = sb / kSubPerChunk;
@@ -203,8 +212,15 @@ descriptor_kernel(DescArgs A) {
     // corners outside its bins like those outside the interior: each of its
     // bins sums the same samples in the same order as a whole-window walk,
     // and a keypoint's longest chain is ~0.6 of the window's.
-    const int hr = PARTS > 1 ? g & 1 : 0;
-    const float rlim_lo = PARTS > 1 ? 2.f * hr - 2.5f : -2.5f, rlim_hi = PARTS > 1 ? 2.f * hr + 0.5f : 2.5f;
+    // (PARTS = 4, shipped: part (hr, hc) also halves the columns the same way,
+    // ~36 % of the window, chain ~0.36;
+    // PARTS = 8: part (rq, hc) owns the row R == rq alone: Rm in {rq - 1, rq},
+    // r_rot in [rq - 2.5, rq - 0.5).)
+    const int hr = PARTS == 4 ? (g >> 1) & 1 : PARTS == 2 ? g & 1 : 0, hc = PARTS >= 4 ? g & 1 : 0;
+    const int rq = PARTS == 8 ? g >> 1 : 0;
+    const float rlim_lo = PARTS == 8 ? rq - 2.5f : PARTS > 1 ? 2.f * hr - 2.5f : -2.5f;
+    const float rlim_hi = PARTS == 8 ? rq - 0.5f : PARTS > 1 ? 2.f * hr + 0.5f : 2.5f;
+    const float clim_lo = PARTS >= 4 ? 2.f * hc - 2.5f : -2.5f, clim_hi = PARTS >= 4 ? 2.f * hc + 0.5f : 2.5f;
     const int k = sord[kslot];
     bool active = k < kend;
     int b = 0, oi = 0, layer = 0;
@@ -270,7 +286,7 @@ descriptor_kernel(DescArgs A) {
         int lo = max(-radius, 1 - px), hi = min(radius, cols - 2 - px);  // 0 < px + j < cols-1
         if (!(py + i > 0 && py + i < rows - 1)) hi = lo - 1;
         slab(sin_t, inv_sin, i * cos_t, lo, hi, rlim_lo, rlim_hi);     // r_rot = j*sin_t + i*cos_t
-        slab(cos_t, inv_cos, -(i * sin_t), lo, hi);                    // c_rot = j*cos_t - i*sin_t
+        slab(cos_t, inv_cos, -(i * sin_t), lo, hi, clim_lo, clim_hi);  // c_rot = j*cos_t - i*sin_t
         const int len = hi >= lo ? hi - lo + 1 : 0;
         rows_tab[g][ri] = (int)(((unsigned)lo << 16) | (unsigned)len);  // |lo| <= 40
         cnt += len;
@@ -441,19 +457,21 @@ descriptor_kernel(DescArgs A) {
       // bin: an exact no-op, every bin is >= +0) instead of going to a trash
       // bin; each weight is masked after every product that uses its
       // unmasked value, so the interior corners' values are unchanged
-      // (PARTS = 2: outside the part's rows R in {2 hr, 2 hr + 1} -- the corner
-      // R = Rm = X - 1 for dr = 0, R = X for dr = 1)
-      const bool r0_in = PARTS > 1 ? (unsigned)(X - 2 * hr - 1) <= 1u : X >= 1;  // Rm >= 0
-      const bool r1_in = PARTS > 1 ? (unsigned)(X - 2 * hr) <= 1u : X <= 3;      // Rm <= 2
+      // (PARTS > 1: outside the part's rows R in {2 hr, 2 hr + 1} -- the corner
+      // R = Rm = X - 1 for dr = 0, R = X for dr = 1 -- and columns likewise)
+      const bool r0_in = PARTS == 8 ? X == rq + 1 : PARTS > 1 ? (unsigned)(X - 2 * hr - 1) <= 1u : X >= 1;  // Rm >= 0
+      const bool r1_in = PARTS == 8 ? X == rq : PARTS > 1 ? (unsigned)(X - 2 * hr) <= 1u : X <= 3;          // Rm <= 2
+      const bool c0_in = PARTS >= 4 ? (unsigned)(Y - 2 * hc - 1) <= 1u : Y >= 1;
+      const bool c1_in = PARTS >= 4 ? (unsigned)(Y - 2 * hc) <= 1u : Y <= 3;
       v_r0 = r0_in ? v_r0 : 0.f;
       v_r1 = r1_in ? v_r1 : 0.f;
       float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
       float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
       // and outside the interior columns
-      v_rc00 = Y >= 1 ? v_rc00 : 0.f;
-      v_rc10 = Y >= 1 ? v_rc10 : 0.f;
-      v_rc01 = Y <= 3 ? v_rc01 : 0.f;
-      v_rc11 = Y <= 3 ? v_rc11 : 0.f;
+      v_rc00 = c0_in ? v_rc00 : 0.f;
+      v_rc10 = c0_in ? v_rc10 : 0.f;
+      v_rc01 = c1_in ? v_rc01 : 0.f;
+      v_rc11 = c1_in ? v_rc11 : 0.f;
       float v[8];
       v[7] = v_rc11 * obin;  // corner index = dr*4 + dc*2 + do, src/sift.cpp:659-672
       v[6] = v_rc11 - v[7];
@@ -659,21 +677,30 @@ descriptor_kernel(DescArgs A) {
     // ---- fold (src/sift.cpp:676-684): read the 16 cells' bins, then write the 128 ----
     float* dv = hist + kslot * (kDescLen + 4);  // the 128-vector reuses histogram storage
     if constexpr (PARTS > 1) {
-      // a part's 8 cells (rows 2 hr, 2 hr + 1): lane q takes cell q whole
-      const int R = 2 * hr + (q >> 2), C = q & 3;
-      float cl[8];
+      // a part's 4 (PARTS = 8: 2) cells: lane q takes one cell and NO = 4 (2)
+      // of its orientations, the first of them adding the two wrap bins
+      // (PARTS = 2: 8 cells, lane q takes cell q whole)
+      constexpr int NO = PARTS == 8 ? 2 : PARTS == 4 ? 4 : 8;
+      const int R = PARTS == 8 ? rq : PARTS == 4 ? 2 * hr + ((q >> 2) & 1) : 2 * hr + (q >> 2);
+      const int C = PARTS == 8 ? 2 * hc + ((q >> 2) & 1) : PARTS == 4 ? 2 * hc + ((q >> 1) & 1) : q & 3;
+      const int oh = PARTS == 8 ? q & 3 : PARTS == 4 ? q & 1 : 0;
+      float cl[NO];
 #pragma unroll
-      for (int o = 0; o < nb + 2; ++o) {
+      for (int u = 0; u < NO; ++u) {
+        const int o = NO * oh + u;
         const int par = ((R & 1) << 2) | ((C & 1) << 1) | (o & 1);
-        const float hv = hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
-        if (o < nb)
-          cl[o] = hv;
-        else
-          cl[o - nb] = cl[o - nb] + hv;
+        cl[u] = hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
+      }
+      if (oh == 0) {
+#pragma unroll
+        for (int o = nb; o < nb + 2; ++o) {
+          const int par = ((R & 1) << 2) | ((C & 1) << 1) | (o & 1);
+          cl[o - nb] = cl[o - nb] + hist[((R >> 1) * 10 + (C >> 1) * 5 + (o >> 1)) * 64 + g * 8 + par];
+        }
       }
       wave_sync_d();
 #pragma unroll
-      for (int t = 0; t < nb; ++t) dv[(R * d + C) * nb + t] = cl[t];
+      for (int u = 0; u < NO; ++u) dv[(R * d + C) * nb + NO * oh + u] = cl[u];
     } else {
       float cell[2][8];
 #pragma unroll
@@ -812,15 +839,18 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
                         const sift_keypoint* kpts, const int* img_kp_off, int batch, int kp_cap,
                         float* desc, int first_octave, int* err_flag, bool detected, int* perm) {
   if (kp_cap <= 0) return;
-  // One image of up to kOneImagePx splits each window over 2 groups (row
-  // halves) and takes its keypoints last first (a layer's windows are larger
-  // than the previous layer's), no ranking pass (8.4 us per 1080p image):
-  // round 6, configs[1]'s descriptor 281 us whole-window (groups of 8, own
-  // order), 207 with 4 parts, 197 + 8 ranked largest first, 182-192 + 8 with 2
-  // parts ranked, 194 with 2 parts last first (217 first first); 8 parts
-  // 238-262 (1.9 x the samples); profiles/r6_desc_one_image_ab.txt,
-  // tools/patches/desc_parts48.patch.
-  const bool rank = !(detected && one_image_variants(L, batch));
+  // One image of up to kOneImagePx splits each window over PARTS groups (row
+  // and column halves) and takes its keypoints last first (a layer's windows
+  // are larger than the previous layer's), no ranking pass (8.4 us per 1080p
+  // image): round 6, configs[1]'s descriptor 281 us whole-window (groups of 8,
+  // own order); resident grids: 207 with 4 parts, 197 + 8 ranked largest
+  // first, 182-192 + 8 with 2 parts ranked, 194 with 2 parts last first (217
+  // first first), 8 parts 238-262 (1.9 x the samples); capacity grids (below):
+  // 2 parts 191, 4 parts 184, 8 parts 220; profiles/r6_desc_one_image_ab.txt.
+#ifndef SIFT_DESC_ONE_RANK
+#define SIFT_DESC_ONE_RANK 0  // A/B builds only: 1 = rank one image too (largest first)
+#endif
+  const bool rank = !(detected && one_image_variants(L, batch)) || SIFT_DESC_ONE_RANK;
   if (rank)
     hipLaunchKernelGGL(desc_rank_kernel, dim3(std::min((kp_cap + kRankChunk - 1) / kRankChunk, 4096)),
                        dim3(kRankChunk), 0, st, kpts, img_kp_off, batch, kp_cap, perm);
@@ -856,6 +886,9 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
 #ifndef SIFT_DESC_ONE_GRID
 #define SIFT_DESC_ONE_GRID 1  // A/B builds only (tools/build_var.sh): 0 = the resident grid
 #endif
+#ifndef SIFT_DESC_ONE_PARTS
+#define SIFT_DESC_ONE_PARTS 4  // A/B builds only (tools/build_var.sh): 1 = whole windows, 2, 4, 8 parts
+#endif
   if (detected && one_image_variants(L, batch) && SIFT_DESC_ONE_GRID)
     // a workgroup per sub-batch of the capacity (waves past the keypoint count
     // exit at once): the dispatcher hands the next sub-batch to whichever wave
@@ -863,12 +896,13 @@ void launch_descriptors(hipStream_t st, const Layout& L, const float2* grad, con
     // 1080p image, round 6)
     // (at most 4 resident grids: a large capacity does not launch empty waves
     // without bound; the kernel strides past its grid)
-    hipLaunchKernelGGL((descriptor_kernel<true, 2, kDescWpe, 2>),
-                       dim3(std::min((kp_cap + 3) / 4,
-                                     4 * resident_grid((const void*)descriptor_kernel<true, 2, kDescWpe, 2>, 64, 0, 8192))),
+    hipLaunchKernelGGL((descriptor_kernel<true, 2, kDescWpe, SIFT_DESC_ONE_PARTS>),
+                       dim3(std::min((kp_cap + kGrp / SIFT_DESC_ONE_PARTS - 1) / (kGrp / SIFT_DESC_ONE_PARTS),
+                                     4 * resident_grid((const void*)descriptor_kernel<true, 2, kDescWpe, SIFT_DESC_ONE_PARTS>,
+                                                       64, 0, 8192))),
                        dim3(64), 0, st, A);
   else if (detected && one_image_variants(L, batch))
-    SIFT_DESC_LAUNCH(true, 2, kDescWpe, 2);
+    SIFT_DESC_LAUNCH(true, 2, kDescWpe, SIFT_DESC_ONE_PARTS);
   else if (detected && batch == 1)
     // one image above kOneImagePx: several resident grids, so that the slots
     // that finish early take the remaining strides (the XCD mapping above
